@@ -1,0 +1,176 @@
+/*
+ * rt_api.h — C-ABI boundary of the MI355X-native path tracer (librt_mi355x.so).
+ *
+ * This header is the drop-in boundary for the reference's accelerated render path.
+ * The reference (Alabuta/RaytracingInOneWeekend) binds its accelerated renderer as
+ *
+ *     extern void cuda_impl(std::uint32_t width, std::uint32_t height,
+ *                           std::vector<math::u8vec3> &image_texels);      // src/main.cxx:18
+ *
+ * defined at src/CUDA/cuda_impl.cu:384-453 and called once at src/main.cxx:114. That
+ * entry has C++ linkage, hardcodes scene/camera/spp/depth and throws on error. The
+ * entry points below replace it with a C ABI: plain pointers and sizes, POD records,
+ * an int status (0 = RT_OK), no exceptions across the boundary, caller-owned host
+ * buffers. The literal `cuda_impl`-shaped C++ drop-in lives in rt_render_impl.hpp.
+ *
+ * Semantics follow the reference CPU render path (src/main.cxx:120-215 with
+ * src/raytracer.hxx, src/camera.hxx, src/math.hxx), not the CUDA variant (whose
+ * different scene/sky/sampling is out of scope).
+ *
+ * Threading: every call is synchronous unless its name ends in _async/_device; one
+ * in-flight render per device. Errors: a negative status; rt_last_error() returns a
+ * thread-local message for the last failing call on this thread.
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_API_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,     /* bad argument (null pointer, zero size, bad index)       */
+    RT_ERR_DEVICE = -2,      /* HIP runtime error (no device, launch/alloc failure)     */
+    RT_ERR_CAPACITY = -3,    /* caller buffer too small                                 */
+    RT_ERR_UNSUPPORTED = -4, /* feature not available in this build / on this host     */
+    RT_ERR_COMM = -5         /* RCCL failure in the multi-GPU path                      */
+};
+
+/* ---- scene records ----------------------------------------------------------------
+ * rt_sphere replaces primitives::sphere {math::vec3 center; float radius;
+ * std::size_t material_index;} (src/primitives.hxx:6-17). A negative radius is legal
+ * and flips the normal (hollow bubble, src/main.cxx:129; src/raytracer.hxx:71).      */
+typedef struct rt_sphere {
+    float center[3];
+    float radius;
+    uint32_t material;
+} rt_sphere;
+
+/* rt_material replaces material::types = std::variant<lambert, metal, dielectric>
+ * (src/material.hxx:12-51). `param` is metal::roughness or dielectric::refraction_index
+ * (unused for lambert).                                                               */
+enum rt_material_kind { RT_LAMBERT = 0, RT_METAL = 1, RT_DIELECTRIC = 2 };
+typedef struct rt_material {
+    uint32_t kind;
+    float albedo[3];
+    float param;
+} rt_material;
+
+/* ---- camera -----------------------------------------------------------------------
+ * Precomputed basis of raytracer::camera (src/camera.hxx:24-44); build it with
+ * rt_camera_init() so the host arithmetic matches the reference constructor bit for bit.
+ * mode RT_CAMERA_REFERENCE reproduces camera::ray() (src/camera.hxx:46-57) as shipped,
+ * whose direction omits "- origin"; RT_CAMERA_CORRECTED subtracts the origin.        */
+enum rt_camera_mode { RT_CAMERA_REFERENCE = 0, RT_CAMERA_CORRECTED = 1 };
+typedef struct rt_camera {
+    float origin[3];
+    float lower_left_corner[3];
+    float horizontal[3];
+    float vertical[3];
+    float lens_radius;
+    uint32_t mode;
+} rt_camera;
+
+/* ---- render parameters ------------------------------------------------------------
+ * width/height: FULL image size (u = x/width, v = y/height as src/main.cxx:192,195).
+ * spp: samples per pixel (app::data::sampling_number, src/main.cxx:23).
+ * max_depth: bounce limit (raytracer::data::bounces_number = 64, src/raytracer.hxx:20).
+ * seed: RNG seed. Each (pixel, sample) owns two PCG32 streams keyed by
+ *       key = (y*width + x)*spp + s — data stream seq 2*seed, camera stream seq 2*seed+1 —
+ *       so any row partition renders the same bits.
+ * Rows rendered: y_i = row_offset + i*row_stride for i in [0, num_rows). num_rows = 0
+ *       means "all rows of the stride pattern below height".
+ * Output layout: row-major RGB f32, 3 floats per pixel. With RT_FLAG_FULL_FRAME the
+ *       output is indexed by the global row y (buffer of height*width*3 floats);
+ *       otherwise rows are packed in render order (num_rows*width*3 floats).          */
+enum rt_flags {
+    RT_FLAG_FULL_FRAME = 1u << 0, /* write rows at their global position             */
+    RT_FLAG_FAST_MATH = 1u << 1,  /* FMA-contracted kernel, stated tolerance          */
+    RT_FLAG_SCALAR_SCENE = 1u << 2 /* read spheres via the scalar cache, not LDS       */
+};
+typedef struct rt_params {
+    uint32_t width, height;
+    uint32_t spp, max_depth;
+    uint64_t seed;
+    uint32_t row_offset, row_stride, num_rows;
+    uint32_t flags;
+} rt_params;
+
+typedef struct rt_stats {
+    uint64_t primaries;  /* pixel-samples traced (W*rows*spp)                          */
+    uint64_t segments;   /* hit_world() calls = ray segments traced                    */
+    uint64_t sphere_tests; /* segments * n_spheres                                     */
+    double kernel_ms;    /* render kernel time (HIP events)                            */
+    double wall_ms;      /* whole call: upload + kernel + download                     */
+} rt_stats;
+
+/* ---- library ----------------------------------------------------------------------- */
+int rt_version(void);
+const char *rt_last_error(void);
+int rt_device_count(int *count);
+
+/* ---- host-side scene / camera construction ----------------------------------------- */
+/* raytracer::camera ctor, src/camera.hxx:24-44 (aperture -> lens_radius = aperture/2). */
+int rt_camera_init(const float position[3], const float lookat[3], const float up[3],
+                   float aspect, float vfov_degrees, float aperture, float focus_distance,
+                   uint32_t mode, rt_camera *out);
+/* The reference's default camera for a width x height image: src/main.cxx:179-183.     */
+int rt_camera_default(uint32_t width, uint32_t height, uint32_t mode, rt_camera *out);
+/* Simple scene, src/main.cxx:120-129: 5 spheres, 4 materials.                          */
+int rt_scene_simple(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres,
+                    rt_material *materials, uint32_t material_cap, uint32_t *n_materials);
+/* Huge random scene: simple scene + the generator of src/main.cxx:131-177 driven by
+ * std::mt19937{seed} (the reference seeds from std::random_device). Namespace typo
+ * fixed; a "type 3" draw pushes no material (as shipped), so such a sphere aliases the
+ * next pushed material and trailing ones are resolved by one default material
+ * (material::types{} = lambert{albedo 1}). Pass null buffers to query the counts.     */
+int rt_scene_huge(uint32_t seed, rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres,
+                  rt_material *materials, uint32_t material_cap, uint32_t *n_materials);
+
+/* ---- synchronous host-buffer renders (the cuda_impl replacement) ------------------- */
+/* Linear (pre-gamma) averaged RGB, f32. rgb_out: see rt_params output layout.          */
+int rt_render_f32(const rt_sphere *spheres, uint32_t n_spheres,
+                  const rt_material *materials, uint32_t n_materials,
+                  const rt_camera *camera, const rt_params *params,
+                  float *rgb_out, rt_stats *stats);
+/* Gamma 1/2.2 + (uint8)(255*c) epilogue (src/main.cxx:39-45,77-85) fused on device.    */
+int rt_render_rgb8(const rt_sphere *spheres, uint32_t n_spheres,
+                   const rt_material *materials, uint32_t n_materials,
+                   const rt_camera *camera, const rt_params *params,
+                   uint8_t *rgb_out, rt_stats *stats);
+/* Row-interleaved split over ngpu devices of this process (device i renders rows
+ * y ≡ i mod ngpu), gathered to device 0 with RCCL over xGMI, then copied to rgb_out
+ * (full frame, height*width*3 floats). ngpu <= 0 uses every visible device.            */
+int rt_render_multi_f32(const rt_sphere *spheres, uint32_t n_spheres,
+                        const rt_material *materials, uint32_t n_materials,
+                        const rt_camera *camera, const rt_params *params, int ngpu,
+                        float *rgb_out, rt_stats *stats);
+
+/* ---- device-resident API (inputs resident in HBM, async on a caller stream) -------- */
+typedef struct rt_scene rt_scene;
+/* Uploads the scene to `device` (packed SoA).                   */
+int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres,
+                    const rt_material *materials, uint32_t n_materials, int device,
+                    rt_scene **out);
+int rt_scene_destroy(rt_scene *scene);
+/* Enqueue one render on `stream` (a hipStream_t, or NULL for the null stream).
+ * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64
+ * that receives the segment count (accumulated; zero it first). No host sync.        */
+int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
+                     float *d_rgb, void *stream, uint64_t *d_segments);
+/* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
+int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,
+                            void *stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* RT_API_H */

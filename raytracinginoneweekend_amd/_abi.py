@@ -1,0 +1,101 @@
+"""ctypes mirror of include/rt_api.h (the C-ABI boundary).
+
+Record layouts are the C structs one for one; numpy dtypes are provided for the arrays
+(spheres, materials) so scenes can be built and inspected without copies.
+"""
+import ctypes as C
+
+import numpy as np
+
+RT_OK = 0
+RT_ERR_INVALID = -1
+RT_ERR_DEVICE = -2
+RT_ERR_CAPACITY = -3
+RT_ERR_UNSUPPORTED = -4
+RT_ERR_COMM = -5
+
+RT_LAMBERT, RT_METAL, RT_DIELECTRIC = 0, 1, 2
+RT_CAMERA_REFERENCE, RT_CAMERA_CORRECTED = 0, 1
+
+RT_FLAG_FULL_FRAME = 1 << 0
+RT_FLAG_FAST_MATH = 1 << 1
+RT_FLAG_SCALAR_SCENE = 1 << 2
+
+
+class RtSphere(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("radius", C.c_float), ("material", C.c_uint32)]
+
+
+class RtMaterial(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("albedo", C.c_float * 3), ("param", C.c_float)]
+
+
+class RtCamera(C.Structure):
+    _fields_ = [
+        ("origin", C.c_float * 3),
+        ("lower_left_corner", C.c_float * 3),
+        ("horizontal", C.c_float * 3),
+        ("vertical", C.c_float * 3),
+        ("lens_radius", C.c_float),
+        ("mode", C.c_uint32),
+    ]
+
+
+class RtParams(C.Structure):
+    _fields_ = [
+        ("width", C.c_uint32), ("height", C.c_uint32),
+        ("spp", C.c_uint32), ("max_depth", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("row_offset", C.c_uint32), ("row_stride", C.c_uint32), ("num_rows", C.c_uint32),
+        ("flags", C.c_uint32),
+    ]
+
+
+class RtStats(C.Structure):
+    _fields_ = [
+        ("primaries", C.c_uint64), ("segments", C.c_uint64), ("sphere_tests", C.c_uint64),
+        ("kernel_ms", C.c_double), ("wall_ms", C.c_double),
+    ]
+
+
+SPHERE_DTYPE = np.dtype([("center", "<f4", (3,)), ("radius", "<f4"), ("material", "<u4")])
+MATERIAL_DTYPE = np.dtype([("kind", "<u4"), ("albedo", "<f4", (3,)), ("param", "<f4")])
+assert SPHERE_DTYPE.itemsize == C.sizeof(RtSphere) == 20
+assert MATERIAL_DTYPE.itemsize == C.sizeof(RtMaterial) == 20
+assert C.sizeof(RtParams) == 40
+
+
+def ptr(arr, ctype=C.c_void_p):
+    """Pointer to a contiguous numpy array's data, typed for a ctypes argument."""
+    assert arr.flags["C_CONTIGUOUS"]
+    return C.cast(arr.ctypes.data, ctype)
+
+
+def rows_of(params):
+    """Number of rows a render covers (rt_params num_rows rule, include/rt_api.h)."""
+    if params.num_rows:
+        return params.num_rows
+    st = params.row_stride or 1
+    if params.row_offset >= params.height:
+        return 0
+    return (params.height - params.row_offset + st - 1) // st
+
+
+def load_scene_file(path):
+    """Scene fixture: 'RTSC' u32 version=1, u32 n_spheres, u32 n_materials, records."""
+    raw = np.fromfile(path, dtype=np.uint8)
+    hdr = raw[:16].view("<u4")
+    if hdr[0] != 0x43535452 or hdr[1] != 1:
+        raise ValueError(f"{path}: not an RTSC v1 scene file")
+    ns, nm = int(hdr[2]), int(hdr[3])
+    s = raw[16:16 + 20 * ns].view(SPHERE_DTYPE).copy()
+    m = raw[16 + 20 * ns:16 + 20 * ns + 20 * nm].view(MATERIAL_DTYPE).copy()
+    return s, m
+
+
+def save_scene_file(path, spheres, materials):
+    hdr = np.array([0x43535452, 1, len(spheres), len(materials)], dtype="<u4")
+    with open(path, "wb") as f:
+        f.write(hdr.tobytes())
+        f.write(np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE).tobytes())
+        f.write(np.ascontiguousarray(materials, dtype=MATERIAL_DTYPE).tobytes())

@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s + frame wall-clock on the huge random-sphere scene, 1280x720 @128spp
+(BASELINE.json config 3), on 1..8 MI355X GPUs.
+
+One step = one full frame: every rank renders its interleaved rows (y = rank + i*N) with
+the HIP megakernel into HBM, the per-rank tiles are gathered to rank 0 over RCCL and
+de-interleaved into the frame. Inputs (scene, camera) are resident in HBM before timing.
+value = W*H*spp primary rays per frame * steps / max-over-ranks time (whole job).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+The cpu_baseline leg (rank 0, N=1) times the REFERENCE's own CPU path (oracle/_ref, built
+from /root/reference) on a bounded row subset of the same workload, on this host's cores.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X f32 vector peak (MI355X_MICROARCH.md, chip-level table)
+FLOP_PER_TEST = 20         # one ray-sphere test, SURVEY.md §8(d): 17 to the discriminant + 3 root
+CONFIGS = {
+    # name: (scene, W, H, spp, depth)
+    "c3": ("huge", 1280, 720, 128, 64),
+    "c2": ("simple", 1280, 720, 64, 50),
+    "c4": ("huge", 3840, 2160, 256, 64),
+    "c5": ("huge", 1280, 720, 1024, 64),
+    "c1": ("simple", 200, 100, 1, 64),
+}
+WORKLOAD = {
+    "c3": "huge-scene 1280x720x128spp (BASELINE config 3)",
+    "c2": "simple-scene 1280x720x64spp depth 50 (config 2)",
+    "c4": "huge-scene 3840x2160x256spp (config 4)",
+    "c5": "huge-scene 1280x720x1024spp (config 5)",
+    "c1": "simple-scene 200x100x1spp (config 1)",
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--camera", default="reference", choices=["reference", "corrected"])
+    ap.add_argument("--variant", default="lds", choices=["lds", "scalar"])
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=32, help="rows in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, camera, seed, rows, threads):
+    """Reference CPU path (oracle/_ref/ref_harness_pcg) on `rows` evenly spaced rows."""
+    scene, W, H, spp, depth = cfg
+    step = max(1, H // rows)
+    nrows = min(rows, (H + step - 1) // step)
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_harness_pcg")
+    sample = f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, {scene} scene, {camera} camera"
+    if os.path.exists(exe):
+        cmd = [exe, "--scene", scene, "--scene-seed", "1234", "--w", str(W), "--h", str(H), "--spp", str(spp),
+               "--depth", str(depth), "--seed", str(seed), "--camera", camera, "--row0", "0",
+               "--row-step", str(step), "--rows", str(nrows), "--threads", str(threads), "--time"]
+        out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
+        r = json.loads(out.strip().splitlines()[-1])
+        return {"value": round(r["mrays_per_s"], 4), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                "sample": sample + f"; {r['seconds']:.1f} s wall"}
+    # fallback: the CPU restatement (bit-identical to the reference, tests/test_oracle_golden.py)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import numpy as np
+    import oracle_binding as O
+    import raytracinginoneweekend_amd as rt
+    s, m = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
+    cam = O.camera_default(W, H, 1 if camera == "corrected" else 0)
+    p = O.make_params(W, H, spp, depth, seed, 0, step, nrows)
+    t0 = time.perf_counter()
+    O.render_f32(s, m, cam, p, threads=threads)
+    sec = time.perf_counter() - t0
+    del np
+    return {"value": round(W * nrows * spp / sec / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": sample + f"; {sec:.1f} s wall"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    distributed = world > 1
+    torch.cuda.set_device(local)
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import raytracinginoneweekend_amd as rt
+    scene_name, W, H, spp, depth = CONFIGS[args.config]
+    arrays = rt.huge_scene_arrays(1234) if scene_name == "huge" else rt.simple_scene_arrays()
+    n_spheres = len(arrays[0])
+    mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
+    cam = rt.Camera.default(W, H, mode)
+    if H % world:
+        raise SystemExit(f"height {H} is not divisible by {world} ranks")
+    rows = H // world
+    params = rt.make_params(W, H, spp, depth, args.seed, row_offset=rank, row_stride=world, num_rows=rows,
+                            scalar_scene=args.variant == "scalar")
+    dev = torch.device("cuda", local)
+    ds = rt.DeviceScene(arrays, device=local)
+    tile = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
+    frame = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if rank == 0 else None
+    gather = [torch.empty_like(tile) for _ in range(world)] if (rank == 0 and distributed) else None
+    seg = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(count_segments):
+        ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
+        if distributed:
+            dist.gather(tile, gather_list=gather, dst=0)
+            if rank == 0:
+                frame.view(rows, world, W, 3).copy_(torch.stack(gather, dim=1))
+        else:
+            frame.copy_(tile)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    seg.zero_()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kt = ds.kernel_times(args.steps)  # render-kernel durations of the timed steps (HIP events)
+    segments = int(seg.item())
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        sg = torch.tensor([segments], dtype=torch.int64, device=dev)
+        dist.all_reduce(sg)
+        segments_all = int(sg.item())
+    else:
+        segments_all = segments
+
+    primaries = W * H * spp * args.steps
+    value = primaries / elapsed / 1e6
+    # roofline of the dominant kernel (render_kernel) on this rank
+    k_avg_ms = sum(kt) / len(kt)
+    flop_per_launch = segments / args.steps * n_spheres * FLOP_PER_TEST
+    achieved = flop_per_launch / (k_avg_ms * 1e-3) / 1e12
+    if rank == 0:
+        rec = {
+            "metric": "Mrays/sec + frame wall-clock, huge-scene 1280x720x128spp @1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference huge scene, std::mt19937 seed 1234; per-sample PCG32 seed %d)" % args.seed,
+            "config": {"workload": WORKLOAD[args.config], "scene": f"{scene_name} ({n_spheres} spheres)",
+                       "width": W, "height": H, "spp": spp, "max_depth": depth, "camera": args.camera,
+                       "kernel": f"exact-{args.variant}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
+            "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
+            "segments_per_primary": round(segments_all / primaries, 4),
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                         "kernel": "render_kernel", "kernel_avg_ms": round(k_avg_ms, 3),
+                         "flop_per_launch": flop_per_launch},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], args.camera, args.seed, args.cpu_rows,
+                                               args.cpu_threads)
+        print(json.dumps(rec), flush=True)
+    ds.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

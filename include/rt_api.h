@@ -165,6 +165,11 @@ int rt_scene_destroy(rt_scene *scene);
  * that receives the segment count (accumulated; zero it first). No host sync.        */
 int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
                      float *d_rgb, void *stream, uint64_t *d_segments);
+/* Durations (ms, HIP events on the render stream) of the render kernel launches of the
+ * most recent calls of rt_render_device on this scene, oldest first: entry i is the sum
+ * over the passes of one call. Writes up to `max` entries, *n = entries written. Waits for
+ * those calls to finish.                                                                */
+int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n);
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,
                             void *stream);

@@ -1,0 +1,58 @@
+// rt_device.h — parameters shared by the host launcher (rt_host.cpp) and the HIP kernels
+// (rt_kernel.hip). Plain C++ POD; no HIP types, so both sides include it.
+#pragma once
+#include <stdint.h>
+
+namespace rt {
+
+// Work decomposition:
+//   pixel enumeration i in [0, n_pixels): the rows of this render (y = row_offset + rr*row_stride),
+//     in 8x8 tiles while both W and the row count allow, row-major for the remainder;
+//   slots: the reference averages samples with libstdc++'s blocked reduce (<numeric>:443-460):
+//     ((c0+c1)+(c2+c3)) per block of 4, blocks added in order, then the spp%4 tail one by one.
+//     Slot k < G4 = spp/4 holds the block sum of samples 4k..4k+3; slot G4+j holds tail sample
+//     4*G4+j. A work item = (slot, pixel): one lane traces its 1 or 4 samples back to back.
+//   items of one launch: slots [slot_begin, slot_end) x all pixels, item I -> slot
+//     slot_begin + I / n_pixels, pixel I % n_pixels. Chunks of 64 consecutive items are
+//     dealt from 8 queues (chunk c belongs to queue c % 8) by per-queue atomic counters.
+struct KParams {
+    // camera basis (rt_camera)
+    float org[3], llc[3], hor[3], ver[3];
+    float lens;
+    uint32_t corrected;
+    // frame
+    uint32_t W, H, spp, max_depth;
+    uint32_t row_offset, row_stride, num_rows;
+    uint32_t full_frame;
+    uint64_t inc_data, inc_cam;  // PCG increments: ((2*seed) << 1) | 1 and ((2*seed+1) << 1) | 1
+    // decomposition
+    uint32_t n_pixels, tiles_x, tiled_rows;  // tiled_rows: rows covered by 8x8 tiles (0 = untiled)
+    uint32_t g4, n_slots;                   // full blocks of 4, total slots
+    uint32_t slot_begin, slot_end;          // this launch's slots
+    uint32_t n_items, n_chunks;
+    // scene
+    uint32_t n_spheres, n_spheres_padded, n_materials;
+    const float *sph_geo;    // [n_spheres_padded][4] = cx, cy, cz, fl(r*r); padding never hits
+    const float *sph_full;   // [n_spheres][4] = cx, cy, cz, r
+    const uint32_t *sph_mat; // [n_spheres]
+    const float *mat_data;   // [n_materials][4] = albedo rgb, param
+    const uint32_t *mat_kind;
+    // outputs / workspace
+    float *slots;            // [slot_end - slot_begin][n_pixels][3]
+    uint32_t *queue_ctr;     // [8]
+    unsigned long long *segments;  // optional
+};
+
+struct KAccum {
+    const float *slots;      // [n_local_slots][n_pixels][3]
+    float *acc;              // [n_pixels][3] running sum between passes
+    float *out;              // final f32 RGB
+    uint8_t *out_u8;         // optional gamma/u8 output (same layout)
+    uint32_t n_pixels, n_local_slots;
+    uint32_t first, last, spp;
+    uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame;
+};
+
+enum Variant : int { V_EXACT_LDS = 0, V_EXACT_SCALAR = 1, V_FAST_LDS = 2 };
+
+} // namespace rt

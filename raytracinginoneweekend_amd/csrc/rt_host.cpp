@@ -1,0 +1,574 @@
+// rt_host.cpp — host side of the C-ABI (include/rt_api.h): scene/camera construction that
+// mirrors the reference's host code bit for bit, device scene upload, pass planning and the
+// render entry points that replace `cuda_impl` (src/main.cxx:18, src/CUDA/cuda_impl.cu:384).
+//
+// Compiled with -ffp-contract=off: the camera basis and the huge-scene generator must round
+// exactly like the reference's (g++, x86-64 SSE, no contraction).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_device.h"
+
+namespace rt {
+hipError_t launch_render(int variant, const KParams &p, uint32_t grid, hipStream_t stream);
+hipError_t occupancy_render(int variant, int *blocks_per_cu, size_t lds);
+hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
+hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_t stream);
+} // namespace rt
+
+namespace {
+
+thread_local std::string g_error;
+
+int fail(int code, const std::string &msg)
+{
+    g_error = msg;
+    return code;
+}
+
+#define RT_HIP(call)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(RT_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- host vector math in the reference's evaluation order (src/math.hxx) ------------
+struct hv { float x, y, z; };
+hv operator+(hv a, hv b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+hv operator-(hv a, hv b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+hv operator*(hv a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+float hlen(hv a) { return std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+hv hnorm(hv a)
+{
+    float l = hlen(a);
+    return std::fabs(l) > FLT_MIN ? hv{a.x / l, a.y / l, a.z / l} : a;
+}
+hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x}; }
+
+constexpr uint32_t kMaxSlotsBytes = 1u << 31;  // slot workspace per pass (2 GiB)
+
+} // namespace
+
+struct rt_scene {
+    int device = 0;
+    uint32_t n_spheres = 0, n_padded = 0, n_materials = 0;
+    float *geo = nullptr, *full = nullptr, *mat_data = nullptr;
+    uint32_t *sph_mat = nullptr, *mat_kind = nullptr;
+    // workspace
+    float *slots = nullptr;
+    size_t slots_bytes = 0;
+    float *acc = nullptr;
+    size_t acc_bytes = 0;
+    uint32_t *queue_ctr = nullptr;
+    int cu_count = 0;
+    int occ_lds = -1, occ_scalar = -1;
+    size_t max_lds = 0;
+    // ring of (start, end) events bracketing the render kernels of each rt_render_device call
+    static constexpr uint32_t kRing = 256;
+    std::vector<hipEvent_t> ev_begin, ev_end;
+    uint64_t calls = 0;
+};
+
+extern "C" {
+
+int rt_version(void) { return RT_API_VERSION; }
+
+const char *rt_last_error(void) { return g_error.c_str(); }
+
+int rt_device_count(int *count)
+{
+    if (!count) return fail(RT_ERR_INVALID, "rt_device_count: null");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return RT_OK;
+}
+
+// raytracer::camera ctor, src/camera.hxx:24-44.
+int rt_camera_init(const float position[3], const float lookat[3], const float up[3], float aspect,
+                   float vfov_degrees, float aperture, float focus_distance, uint32_t mode, rt_camera *out)
+{
+    if (!position || !lookat || !up || !out) return fail(RT_ERR_INVALID, "rt_camera_init: null argument");
+    if (mode > RT_CAMERA_CORRECTED) return fail(RT_ERR_INVALID, "rt_camera_init: bad mode");
+    const hv P{position[0], position[1], position[2]}, L{lookat[0], lookat[1], lookat[2]}, U{up[0], up[1], up[2]};
+    const float theta = (vfov_degrees * static_cast<float>(0.01745329251994329576923690768489)) / 2.f; // math.hxx:8-13
+    const float height = std::tan(theta);
+    const float width = height * aspect;
+    const hv w = hnorm(P - L);
+    const hv u = hnorm(hcross(U, w));
+    const hv v = hnorm(hcross(w, u));
+    const hv llc = P - ((u * width + v * height) + w) * focus_distance;
+    const hv hor = ((u * width) * focus_distance) * 2.f;
+    const hv ver = ((v * height) * focus_distance) * 2.f;
+    rt_camera c{};
+    c.origin[0] = P.x; c.origin[1] = P.y; c.origin[2] = P.z;
+    c.lower_left_corner[0] = llc.x; c.lower_left_corner[1] = llc.y; c.lower_left_corner[2] = llc.z;
+    c.horizontal[0] = hor.x; c.horizontal[1] = hor.y; c.horizontal[2] = hor.z;
+    c.vertical[0] = ver.x; c.vertical[1] = ver.y; c.vertical[2] = ver.z;
+    c.lens_radius = aperture / 2.f;
+    c.mode = mode;
+    *out = c;
+    return RT_OK;
+}
+
+// src/main.cxx:179-183
+int rt_camera_default(uint32_t width, uint32_t height, uint32_t mode, rt_camera *out)
+{
+    if (!width || !height) return fail(RT_ERR_INVALID, "rt_camera_default: zero size");
+    const float pos[3] = {-4.f, 3.2f, 5.f}, look[3] = {0.f, 1.f, 0.f}, up[3] = {0.f, 1.f, 0.f};
+    const float focus = hlen(hv{pos[0], pos[1], pos[2]} - hv{look[0], look[1], look[2]});
+    return rt_camera_init(pos, look, up, static_cast<float>(width) / static_cast<float>(height), 42.f, 0.0625f,
+                          focus, mode, out);
+}
+
+} // extern "C"
+
+namespace {
+
+struct scene_builder {
+    std::vector<rt_sphere> s;
+    std::vector<rt_material> m;
+    void mat(uint32_t kind, float r, float g, float b, float param) { m.push_back({kind, {r, g, b}, param}); }
+    void sph(float x, float y, float z, float radius, uint32_t mi) { s.push_back({{x, y, z}, radius, mi}); }
+    void simple()  // src/main.cxx:120-129
+    {
+        mat(RT_LAMBERT, static_cast<float>(.1), static_cast<float>(.2), static_cast<float>(.5), 0.f);
+        mat(RT_METAL, static_cast<float>(.8), static_cast<float>(.6), static_cast<float>(.2), 0.f);
+        mat(RT_DIELECTRIC, 1.f, 1.f, 1.f, 1.5f);
+        mat(RT_LAMBERT, static_cast<float>(.64), static_cast<float>(.8), static_cast<float>(.0), 0.f);
+        sph(0.f, 1.f, 0.f, 1.f, 0);
+        sph(0.f, -1000.125f, 0.f, 1000.f, 3);
+        sph(2.f, 1.f, 0.f, 1.f, 1);
+        sph(-2.f, 1.f, 0.f, 1.f, 2);
+        sph(-2.f, 1.f, 0.f, -.99f, 2);
+    }
+    // src/main.cxx:131-177 (namespace typo fixed). Draw order: type, center.x, center.z, then
+    // the material's draws; a type-3 sphere pushes no material, so it shares the index of the
+    // next pushed one and trailing ones are resolved by default materials (lambert, albedo 1).
+    void huge(uint32_t seed)
+    {
+        simple();
+        std::mt19937 gen{seed};
+        std::uniform_int_distribution<int> rd_int{0, 3};
+        std::uniform_real_distribution<float> rd_real{0.f, 1.f};
+        for (int a = -11; a < 11; ++a) {
+            for (int b = -11; b < 11; ++b) {
+                const int type = rd_int(gen);
+                const float cx = .9f * rd_real(gen) + static_cast<float>(a);
+                const float cz = .9f * rd_real(gen) + static_cast<float>(b);
+                if (hlen(hv{cx, .2f, cz} - hv{0.f, 1.f, 0.f}) < 1.f) continue;
+                sph(cx, .2f, cz, .2f, static_cast<uint32_t>(m.size()));
+                if (type == 0) {
+                    const float r = rd_real(gen), g = rd_real(gen), bb = rd_real(gen);
+                    mat(RT_LAMBERT, r, g, bb, 0.f);
+                } else if (type == 1) {
+                    const float r = rd_real(gen), g = rd_real(gen), bb = rd_real(gen);
+                    const float rough = .5f * rd_real(gen);
+                    mat(RT_METAL, r, g, bb, rough);
+                } else if (type == 2) {
+                    const float r = rd_real(gen), g = rd_real(gen), bb = rd_real(gen);
+                    mat(RT_DIELECTRIC, r, g, bb, 1.5f);
+                }
+            }
+        }
+        uint32_t need = 0;
+        for (auto &x : s) need = std::max(need, x.material + 1u);
+        while (m.size() < need) mat(RT_LAMBERT, 1.f, 1.f, 1.f, 0.f);
+    }
+    int emit(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres, rt_material *materials,
+             uint32_t material_cap, uint32_t *n_materials) const
+    {
+        if (n_spheres) *n_spheres = static_cast<uint32_t>(s.size());
+        if (n_materials) *n_materials = static_cast<uint32_t>(m.size());
+        if (spheres) {
+            if (sphere_cap < s.size()) return fail(RT_ERR_CAPACITY, "scene: sphere buffer too small");
+            std::memcpy(spheres, s.data(), s.size() * sizeof(rt_sphere));
+        }
+        if (materials) {
+            if (material_cap < m.size()) return fail(RT_ERR_CAPACITY, "scene: material buffer too small");
+            std::memcpy(materials, m.data(), m.size() * sizeof(rt_material));
+        }
+        return RT_OK;
+    }
+};
+
+uint32_t rows_of(const rt_params &p)
+{
+    if (p.num_rows) return p.num_rows;
+    const uint32_t st = p.row_stride ? p.row_stride : 1;
+    return p.row_offset >= p.height ? 0 : (p.height - p.row_offset + st - 1) / st;
+}
+
+int check_params(const rt_params *p)
+{
+    if (!p) return fail(RT_ERR_INVALID, "params: null");
+    if (!p->width || !p->height || !p->spp) return fail(RT_ERR_INVALID, "params: width, height and spp must be > 0");
+    const uint32_t st = p->row_stride ? p->row_stride : 1;
+    const uint32_t rows = rows_of(*p);
+    if (rows && static_cast<uint64_t>(p->row_offset) + static_cast<uint64_t>(rows - 1) * st >= p->height)
+        return fail(RT_ERR_INVALID, "params: rows exceed the image height");
+    if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE))
+        return fail(RT_ERR_INVALID, "params: unknown flag");
+    if (p->flags & RT_FLAG_FAST_MATH) return fail(RT_ERR_UNSUPPORTED, "params: fast-math kernel not built yet");
+    return RT_OK;
+}
+
+int ensure(void **ptr, size_t *have, size_t want)
+{
+    if (*have >= want && *ptr) return RT_OK;
+    if (*ptr) {
+        RT_HIP(hipDeviceSynchronize());
+        RT_HIP(hipFree(*ptr));
+        *ptr = nullptr;
+        *have = 0;
+    }
+    RT_HIP(hipMalloc(ptr, std::max<size_t>(want, 256)));
+    *have = want;
+    return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_scene_simple(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres, rt_material *materials,
+                    uint32_t material_cap, uint32_t *n_materials)
+{
+    scene_builder b;
+    b.simple();
+    return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
+}
+
+int rt_scene_huge(uint32_t seed, rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres,
+                  rt_material *materials, uint32_t material_cap, uint32_t *n_materials)
+{
+    scene_builder b;
+    b.huge(seed);
+    return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
+}
+
+int rt_scene_destroy(rt_scene *sc)
+{
+    if (!sc) return RT_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(sc->device);
+    for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
+    for (auto e : sc->ev_end) (void)hipEventDestroy(e);
+    for (void *p : {(void *)sc->geo, (void *)sc->full, (void *)sc->mat_data, (void *)sc->sph_mat,
+                    (void *)sc->mat_kind, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
+        if (p) (void)hipFree(p);
+    (void)hipSetDevice(prev);
+    delete sc;
+    return RT_OK;
+}
+
+int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
+                    uint32_t n_materials, int device, rt_scene **out)
+{
+    if (!out || (n_spheres && !spheres) || !materials || !n_materials)
+        return fail(RT_ERR_INVALID, "rt_scene_create: null argument or no materials");
+    *out = nullptr;
+    for (uint32_t i = 0; i < n_spheres; ++i)
+        if (spheres[i].material >= n_materials)
+            return fail(RT_ERR_INVALID, "rt_scene_create: sphere " + std::to_string(i) + " has material index " +
+                                            std::to_string(spheres[i].material) + " >= " + std::to_string(n_materials));
+    for (uint32_t i = 0; i < n_materials; ++i)
+        if (materials[i].kind > RT_DIELECTRIC)
+            return fail(RT_ERR_INVALID, "rt_scene_create: material " + std::to_string(i) + " has unknown kind");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_DEVICE, "rt_scene_create: no HIP device");
+    if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "rt_scene_create: bad device index");
+    RT_HIP(hipSetDevice(device));
+
+    // Packed device layout: geo = {cx, cy, cz, fl(r*r)} padded to a multiple
+    // of 4 with never-hit entries (r*r = -inf makes the discriminant -inf or NaN).
+    const uint32_t padded = (n_spheres + 3u) & ~3u;
+    std::vector<float> geo(static_cast<size_t>(std::max(padded, 4u)) * 4, 0.f), full(std::max(n_spheres, 1u) * 4, 0.f);
+    std::vector<uint32_t> smat(std::max(n_spheres, 1u), 0u), kind(n_materials);
+    std::vector<float> md(static_cast<size_t>(n_materials) * 4);
+    for (uint32_t i = 0; i < padded; ++i) {
+        if (i < n_spheres) {
+            const rt_sphere &s = spheres[i];
+            geo[4 * i] = s.center[0]; geo[4 * i + 1] = s.center[1]; geo[4 * i + 2] = s.center[2];
+            geo[4 * i + 3] = s.radius * s.radius;  // raytracer.hxx:58
+            full[4 * i] = s.center[0]; full[4 * i + 1] = s.center[1]; full[4 * i + 2] = s.center[2];
+            full[4 * i + 3] = s.radius;
+            smat[i] = s.material;
+        } else {
+            geo[4 * i + 3] = -INFINITY;
+        }
+    }
+    for (uint32_t i = 0; i < n_materials; ++i) {
+        kind[i] = materials[i].kind;
+        md[4 * i] = materials[i].albedo[0]; md[4 * i + 1] = materials[i].albedo[1]; md[4 * i + 2] = materials[i].albedo[2];
+        md[4 * i + 3] = materials[i].param;
+    }
+    rt_scene *sc = new rt_scene();
+    sc->device = device;
+    sc->n_spheres = n_spheres;
+    sc->n_padded = padded;
+    sc->n_materials = n_materials;
+    auto up = [&](void **dst, const void *src, size_t bytes) -> int {
+        RT_HIP(hipMalloc(dst, bytes));
+        RT_HIP(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+        return RT_OK;
+    };
+    int rc = RT_OK;
+    if (rc == RT_OK) rc = up((void **)&sc->geo, geo.data(), geo.size() * 4);
+    if (rc == RT_OK) rc = up((void **)&sc->full, full.data(), full.size() * 4);
+    if (rc == RT_OK) rc = up((void **)&sc->sph_mat, smat.data(), smat.size() * 4);
+    if (rc == RT_OK) rc = up((void **)&sc->mat_data, md.data(), md.size() * 4);
+    if (rc == RT_OK) rc = up((void **)&sc->mat_kind, kind.data(), kind.size() * 4);
+    if (rc == RT_OK) {
+        hipError_t e = hipMalloc((void **)&sc->queue_ctr, 8 * sizeof(uint32_t));
+        if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    if (rc == RT_OK) {
+        hipDeviceProp_t prop;
+        hipError_t e = hipGetDeviceProperties(&prop, device);
+        if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipGetDeviceProperties: ") + hipGetErrorString(e));
+        else {
+            sc->cu_count = prop.multiProcessorCount;
+            sc->max_lds = prop.sharedMemPerBlock;
+        }
+    }
+    for (uint32_t i = 0; rc == RT_OK && i < rt_scene::kRing; ++i) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+            if (a) (void)hipEventDestroy(a);
+            rc = fail(RT_ERR_DEVICE, "hipEventCreate failed");
+            break;
+        }
+        sc->ev_begin.push_back(a);
+        sc->ev_end.push_back(b);
+    }
+    if (rc != RT_OK) {
+        rt_scene_destroy(sc);
+        return rc;
+    }
+    *out = sc;
+    return RT_OK;
+}
+
+int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *params, float *d_rgb, void *stream,
+                     uint64_t *d_segments)
+{
+    if (!sc || !camera || !d_rgb) return fail(RT_ERR_INVALID, "rt_render_device: null argument");
+    if (int rc = check_params(params); rc != RT_OK) return rc;
+    const rt_params P = *params;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    RT_HIP(hipSetDevice(sc->device));
+
+    rt::KParams k{};
+    for (int c = 0; c < 3; ++c) {
+        k.org[c] = camera->origin[c];
+        k.llc[c] = camera->lower_left_corner[c];
+        k.hor[c] = camera->horizontal[c];
+        k.ver[c] = camera->vertical[c];
+    }
+    k.lens = camera->lens_radius;
+    k.corrected = camera->mode == RT_CAMERA_CORRECTED;
+    k.W = P.width;
+    k.H = P.height;
+    k.spp = P.spp;
+    k.max_depth = P.max_depth;
+    k.row_offset = P.row_offset;
+    k.row_stride = P.row_stride ? P.row_stride : 1;
+    k.num_rows = rows_of(P);
+    k.full_frame = (P.flags & RT_FLAG_FULL_FRAME) ? 1u : 0u;
+    k.inc_data = ((2ull * P.seed) << 1u) | 1ull;
+    k.inc_cam = ((2ull * P.seed + 1ull) << 1u) | 1ull;
+    const uint64_t n_pixels = static_cast<uint64_t>(P.width) * k.num_rows;
+    if (n_pixels == 0) return RT_OK;
+    if (n_pixels >= (1ull << 31)) return fail(RT_ERR_INVALID, "rt_render_device: more than 2^31 pixels in one call");
+    k.n_pixels = static_cast<uint32_t>(n_pixels);
+    const bool tiled = (P.width % 8u) == 0u;
+    k.tiles_x = tiled ? P.width / 8u : 1u;
+    k.tiled_rows = tiled ? (k.num_rows / 8u) * 8u : 0u;
+    k.g4 = P.spp / 4u;
+    k.n_slots = k.g4 + P.spp % 4u;
+    k.n_spheres = sc->n_spheres;
+    k.n_spheres_padded = sc->n_padded;
+    k.n_materials = sc->n_materials;
+    k.sph_geo = sc->geo;
+    k.sph_full = sc->full;
+    k.sph_mat = sc->sph_mat;
+    k.mat_data = sc->mat_data;
+    k.mat_kind = sc->mat_kind;
+    k.queue_ctr = sc->queue_ctr;
+    k.segments = reinterpret_cast<unsigned long long *>(d_segments);
+
+    int variant = (P.flags & RT_FLAG_SCALAR_SCENE) ? rt::V_EXACT_SCALAR : rt::V_EXACT_LDS;
+    const size_t lds = static_cast<size_t>(sc->n_padded) * 16u;
+    if (variant == rt::V_EXACT_LDS && lds > sc->max_lds) variant = rt::V_EXACT_SCALAR;
+    int &occ = variant == rt::V_EXACT_LDS ? sc->occ_lds : sc->occ_scalar;
+    if (occ < 0) {
+        RT_HIP(rt::occupancy_render(variant, &occ, variant == rt::V_EXACT_LDS ? lds : 0));
+        occ = std::max(occ, 1);
+    }
+
+    // pass planning: the slot workspace of one pass stays under kMaxSlotsBytes
+    const uint64_t per_slot = n_pixels * 12ull;
+    uint32_t slots_per_pass = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(k.n_slots, kMaxSlotsBytes / per_slot)));
+    slots_per_pass = static_cast<uint32_t>(std::min<uint64_t>(slots_per_pass, ((1ull << 31) - 64) / n_pixels));
+    if (int rc = ensure((void **)&sc->slots, &sc->slots_bytes, per_slot * slots_per_pass); rc) return rc;
+    if (slots_per_pass < k.n_slots)
+        if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_slot); rc) return rc;
+    k.slots = sc->slots;
+
+    const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
+    ++sc->calls;
+    for (uint32_t s0 = 0; s0 < k.n_slots; s0 += slots_per_pass) {
+        const uint32_t s1 = std::min(k.n_slots, s0 + slots_per_pass);
+        k.slot_begin = s0;
+        k.slot_end = s1;
+        k.n_items = static_cast<uint32_t>(n_pixels * (s1 - s0));
+        k.n_chunks = (k.n_items + 63u) / 64u;
+        const uint32_t grid = static_cast<uint32_t>(
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_chunks + 3u) / 4u)));
+        RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * sizeof(uint32_t), st));
+        if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
+        RT_HIP(rt::launch_render(variant, k, grid, st));
+        if (s1 == k.n_slots) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
+        rt::KAccum a{};
+        a.slots = sc->slots;
+        a.acc = sc->acc;
+        a.out = d_rgb;
+        a.out_u8 = nullptr;
+        a.n_pixels = k.n_pixels;
+        a.n_local_slots = s1 - s0;
+        a.first = s0 == 0;
+        a.last = s1 == k.n_slots;
+        a.spp = P.spp;
+        a.W = P.width;
+        a.tiles_x = k.tiles_x;
+        a.tiled_rows = k.tiled_rows;
+        a.row_offset = k.row_offset;
+        a.row_stride = k.row_stride;
+        a.full_frame = k.full_frame;
+        RT_HIP(rt::launch_accumulate(a, st));
+    }
+    return RT_OK;
+}
+
+int rt_scene_kernel_times(rt_scene *sc, uint32_t max, float *ms, uint32_t *n)
+{
+    if (!sc || !n || (max && !ms)) return fail(RT_ERR_INVALID, "rt_scene_kernel_times: null argument");
+    const uint64_t avail = std::min<uint64_t>(sc->calls, rt_scene::kRing);
+    const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(avail, max));
+    RT_HIP(hipSetDevice(sc->device));
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const uint32_t r = static_cast<uint32_t>((sc->calls - cnt + i) % rt_scene::kRing);
+        RT_HIP(hipEventSynchronize(sc->ev_end[r]));
+        RT_HIP(hipEventElapsedTime(ms + i, sc->ev_begin[r], sc->ev_end[r]));
+    }
+    *n = cnt;
+    return RT_OK;
+}
+
+int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels, void *stream)
+{
+    if (!d_rgb || !d_out) return fail(RT_ERR_INVALID, "rt_epilogue_rgb8_device: null argument");
+    if (!n_pixels) return RT_OK;
+    RT_HIP(rt::launch_epilogue(d_rgb, d_out, n_pixels * 3u, static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+} // extern "C"
+
+namespace {
+
+// Synchronous host-buffer render on the current device (the cuda_impl replacement).
+int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
+                const rt_camera *camera, const rt_params *params, float *rgb_out, uint8_t *u8_out, rt_stats *stats)
+{
+    if (!camera || (!rgb_out && !u8_out)) return fail(RT_ERR_INVALID, "render: null argument");
+    if (int rc = check_params(params); rc != RT_OK) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    int dev = 0;
+    RT_HIP(hipGetDevice(&dev));
+    rt_scene *sc = nullptr;
+    if (int rc = rt_scene_create(spheres, n_spheres, materials, n_materials, dev, &sc); rc) return rc;
+    const rt_params &P = *params;
+    const uint64_t rows = (P.flags & RT_FLAG_FULL_FRAME) ? P.height : rows_of(P);
+    const uint64_t n_values = rows * P.width * 3u;
+    float *d_rgb = nullptr;
+    uint8_t *d_u8 = nullptr;
+    uint64_t *d_seg = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = RT_OK;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+        return rc == RT_OK;
+    };
+    if (chk(hipMalloc((void **)&d_rgb, n_values * 4), "hipMalloc") && u8_out) chk(hipMalloc((void **)&d_u8, n_values), "hipMalloc");
+    if (rc == RT_OK) chk(hipMalloc((void **)&d_seg, 8), "hipMalloc");
+    if (rc == RT_OK && (P.flags & RT_FLAG_FULL_FRAME)) chk(hipMemset(d_rgb, 0, n_values * 4), "hipMemset");
+    if (rc == RT_OK) chk(hipMemset(d_seg, 0, 8), "hipMemset");
+    if (rc == RT_OK) chk(hipEventCreate(&e0), "hipEventCreate");
+    if (rc == RT_OK) chk(hipEventCreate(&e1), "hipEventCreate");
+    if (rc == RT_OK) chk(hipEventRecord(e0, nullptr), "hipEventRecord");
+    if (rc == RT_OK) rc = rt_render_device(sc, camera, params, d_rgb, nullptr, d_seg);
+    if (rc == RT_OK) chk(hipEventRecord(e1, nullptr), "hipEventRecord");
+    if (rc == RT_OK && u8_out) rc = rt_epilogue_rgb8_device(d_rgb, d_u8, n_values / 3, nullptr);
+    if (rc == RT_OK) chk(hipDeviceSynchronize(), "render");
+    uint64_t segs = 0;
+    float ms = 0.f;
+    if (rc == RT_OK && rgb_out) chk(hipMemcpy(rgb_out, d_rgb, n_values * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == RT_OK && u8_out) chk(hipMemcpy(u8_out, d_u8, n_values, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == RT_OK) chk(hipMemcpy(&segs, d_seg, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == RT_OK) chk(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (d_rgb) (void)hipFree(d_rgb);
+    if (d_u8) (void)hipFree(d_u8);
+    if (d_seg) (void)hipFree(d_seg);
+    rt_scene_destroy(sc);
+    if (rc == RT_OK && stats) {
+        stats->primaries = static_cast<uint64_t>(P.width) * rows_of(P) * P.spp;
+        stats->segments = segs;
+        stats->sphere_tests = segs * n_spheres;
+        stats->kernel_ms = ms;
+        stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return rc;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_render_f32(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
+                  const rt_camera *camera, const rt_params *params, float *rgb_out, rt_stats *stats)
+{
+    if (!rgb_out) return fail(RT_ERR_INVALID, "rt_render_f32: null output");
+    return render_host(spheres, n_spheres, materials, n_materials, camera, params, rgb_out, nullptr, stats);
+}
+
+int rt_render_rgb8(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
+                   const rt_camera *camera, const rt_params *params, uint8_t *rgb_out, rt_stats *stats)
+{
+    if (!rgb_out) return fail(RT_ERR_INVALID, "rt_render_rgb8: null output");
+    return render_host(spheres, n_spheres, materials, n_materials, camera, params, nullptr, rgb_out, stats);
+}
+
+int rt_render_multi_f32(const rt_sphere *, uint32_t, const rt_material *, uint32_t, const rt_camera *,
+                        const rt_params *, int, float *, rt_stats *)
+{
+    return fail(RT_ERR_UNSUPPORTED, "rt_render_multi_f32: not built yet");
+}
+
+} // extern "C"

@@ -1,0 +1,122 @@
+"""Render entry points over the C-ABI (the replacement for `cuda_impl`, src/main.cxx:18,114).
+
+render_f32 / render_rgb8   synchronous, host numpy buffers (rt_render_f32 / rt_render_rgb8)
+DeviceScene.render         async on a caller stream into a device buffer (rt_render_device),
+                           the path bench.py times with inputs resident in HBM
+save_ppm                   app::save_to_file (src/main.cxx:87-101)
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi as abi
+from ._lib import check, lib
+from .camera import Camera
+
+
+def make_params(width, height, spp, max_depth=64, seed=1234, row_offset=0, row_stride=1, num_rows=0,
+                full_frame=False, scalar_scene=False, fast_math=False):
+    flags = (abi.RT_FLAG_FULL_FRAME if full_frame else 0) | (abi.RT_FLAG_SCALAR_SCENE if scalar_scene else 0) \
+        | (abi.RT_FLAG_FAST_MATH if fast_math else 0)
+    return abi.RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, num_rows, flags)
+
+
+def _scene_arrays(scene):
+    if isinstance(scene, tuple):
+        s, m = scene
+    else:
+        s, m = scene.arrays()
+    return (np.ascontiguousarray(s, dtype=abi.SPHERE_DTYPE), np.ascontiguousarray(m, dtype=abi.MATERIAL_DTYPE))
+
+
+def _cam(camera, params):
+    if camera is None:
+        return Camera.default(params.width, params.height).c
+    return camera.c if isinstance(camera, Camera) else camera
+
+
+def _out_rows(params):
+    return params.height if params.flags & abi.RT_FLAG_FULL_FRAME else abi.rows_of(params)
+
+
+def render_f32(scene, params, camera=None):
+    """Averaged linear RGB (before gamma) as float32 (rows, width, 3); returns (image, stats)."""
+    s, m = _scene_arrays(scene)
+    out = np.zeros((_out_rows(params), params.width, 3), dtype=np.float32)
+    st = abi.RtStats()
+    check(lib().rt_render_f32(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s), abi.ptr(m, C.POINTER(abi.RtMaterial)),
+                              len(m), C.byref(_cam(camera, params)), C.byref(params),
+                              abi.ptr(out, C.POINTER(C.c_float)), C.byref(st)))
+    return out, st
+
+
+def render_rgb8(scene, params, camera=None):
+    """Gamma-corrected 8-bit RGB (rows, width, 3), as main.cxx:209-213 produces."""
+    s, m = _scene_arrays(scene)
+    out = np.zeros((_out_rows(params), params.width, 3), dtype=np.uint8)
+    st = abi.RtStats()
+    check(lib().rt_render_rgb8(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s), abi.ptr(m, C.POINTER(abi.RtMaterial)),
+                               len(m), C.byref(_cam(camera, params)), C.byref(params),
+                               abi.ptr(out, C.POINTER(C.c_uint8)), C.byref(st)))
+    return out, st
+
+
+def render_multi_f32(scene, params, ngpu=0, camera=None):
+    """Row-interleaved render over `ngpu` devices of this process, gathered with RCCL."""
+    s, m = _scene_arrays(scene)
+    out = np.zeros((params.height, params.width, 3), dtype=np.float32)
+    st = abi.RtStats()
+    check(lib().rt_render_multi_f32(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
+                                    abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), C.byref(_cam(camera, params)),
+                                    C.byref(params), ngpu, abi.ptr(out, C.POINTER(C.c_float)), C.byref(st)))
+    return out, st
+
+
+class DeviceScene:
+    """A scene resident in HBM on one device (rt_scene_create); renders are stream-ordered."""
+
+    def __init__(self, scene, device=0):
+        s, m = _scene_arrays(scene)
+        self.n_spheres, self.n_materials = len(s), len(m)
+        h = C.c_void_p()
+        check(lib().rt_scene_create(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
+                                    abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), device, C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def render(self, camera, params, d_rgb, stream=None, d_segments=None):
+        """Enqueue a render into device pointer d_rgb (int address) on `stream` (int handle)."""
+        check(lib().rt_render_device(self.handle, C.byref(_cam(camera, params)), C.byref(params),
+                                     C.c_void_p(d_rgb), C.c_void_p(stream or 0),
+                                     C.c_void_p(d_segments) if d_segments else None))
+
+    def kernel_times(self, max_calls=256):
+        """Render-kernel durations (ms) of the most recent render() calls, oldest first."""
+        buf = (C.c_float * max_calls)()
+        n = C.c_uint32(0)
+        check(lib().rt_scene_kernel_times(self.handle, max_calls, buf, C.byref(n)))
+        return list(buf[:n.value])
+
+    def close(self):
+        if self.handle:
+            lib().rt_scene_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def epilogue_rgb8_device(d_rgb, d_out, n_pixels, stream=None):
+    check(lib().rt_epilogue_rgb8_device(C.c_void_p(d_rgb), C.c_void_p(d_out), n_pixels, C.c_void_p(stream or 0)))
+
+
+def save_ppm(path, rgb8):
+    """app::save_to_file: binary P6, 'P6\\n<w> <h>\\n255\\n' then texels (src/main.cxx:87-101)."""
+    rgb8 = np.ascontiguousarray(rgb8, dtype=np.uint8)
+    h, w, _ = rgb8.shape
+    with open(path, "wb") as f:
+        f.write(f"P6\n{w} {h}\n255\n".encode())
+        f.write(rgb8.tobytes())

@@ -1,0 +1,125 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/rt_api.h
+declares, and its host code (scene generator, camera basis, argument validation) matches
+the reference. No compute call needs a GPU here.
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import golden_io as G
+import oracle_binding as O
+import raytracinginoneweekend_amd as rt
+from raytracinginoneweekend_amd import _abi as abi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(REPO, "include", "rt_api.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = rt.lib()
+    declared = _declared_symbols()
+    assert len(declared) >= 14
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    from raytracinginoneweekend_amd import _lib
+    assert set(declared) == set(_lib.EXPORTS), "ctypes declarations out of sync with rt_api.h"
+
+
+def test_version():
+    assert rt.lib().rt_version() == 1
+
+
+def test_huge_scene_generator_matches_reference():
+    s, m = rt.huge_scene_arrays(1234)
+    gs, gm = G.scene("huge")
+    assert len(s) == 486
+    assert s.tobytes() == gs.tobytes() and m.tobytes() == gm.tobytes()
+    # every index resolves (the reference's type-3 draws leave dangling indices otherwise)
+    assert s["material"].max() < len(m)
+
+
+def test_simple_scene_matches_reference():
+    s, m = rt.simple_scene_arrays()
+    gs, gm = G.scene("simple")
+    assert s.tobytes() == gs.tobytes() and m.tobytes() == gm.tobytes()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 7, 99])
+def test_huge_scene_other_seeds_well_formed(seed):
+    s, m = rt.huge_scene_arrays(seed)
+    assert 480 <= len(s) <= 490
+    assert (s["radius"][5:] == np.float32(0.2)).all()
+    assert s["material"].max() < len(m)
+    assert set(np.unique(m["kind"])) <= {0, 1, 2}
+
+
+@pytest.mark.parametrize("W,H,mode", [(200, 100, 0), (1280, 720, 0), (3840, 2160, 1), (37, 19, 1)])
+def test_camera_basis_matches_oracle(W, H, mode):
+    assert bytes(rt.Camera.default(W, H, mode).c) == bytes(O.camera_default(W, H, mode))
+
+
+def test_camera_init_custom():
+    cam = rt.Camera((1, 2, 3), (0, 0, -1), (0, 1, 0), 1.5, 60.0, 0.5, 2.0, rt.CORRECTED)
+    ref = abi.RtCamera()
+    f3 = C.c_float * 3
+    O.lib().oracle_camera_init(f3(1, 2, 3), f3(0, 0, -1), f3(0, 1, 0), 1.5, 60.0, 0.5, 2.0, 1, C.byref(ref))
+    assert bytes(cam.c) == bytes(ref)
+    assert cam.basis()["lens_radius"] == 0.25
+
+
+def test_invalid_arguments_fail_loudly():
+    s, m = rt.simple_scene_arrays()
+    with pytest.raises(rt.RtError) as e:
+        rt.render_f32((s, m), rt.make_params(0, 10, 1))
+    assert e.value.status == abi.RT_ERR_INVALID
+    with pytest.raises(rt.RtError):
+        rt.render_f32((s, m), rt.make_params(10, 10, 0))
+    with pytest.raises(rt.RtError):  # rows past the bottom of the image
+        rt.render_f32((s, m), rt.make_params(10, 10, 1, row_offset=5, num_rows=6))
+    bad = s.copy()
+    bad["material"][0] = 99
+    with pytest.raises(rt.RtError) as e:
+        rt.DeviceScene((bad, m))
+    assert "material index" in str(e.value)
+    with pytest.raises(rt.RtError):
+        rt.Camera.default(0, 10)
+
+
+def test_scene_capacity_error():
+    n = C.c_uint32(0)
+    buf = np.zeros(2, dtype=abi.SPHERE_DTYPE)
+    rc = rt.lib().rt_scene_simple(abi.ptr(buf, C.POINTER(abi.RtSphere)), 2, C.byref(n), None, 0, None)
+    assert rc == abi.RT_ERR_CAPACITY and n.value == 5
+    assert b"too small" in rt.lib().rt_last_error()
+
+
+def test_raytracer_data_roundtrip():
+    d = rt.RaytracerData()
+    d.add_material(rt.Lambert((.1, .2, .5)))
+    d.add_material(rt.Metal((.8, .6, .2), 0))
+    d.add_material(rt.Dielectric(1, 1.5))
+    d.add_material(rt.Lambert((.64, .8, .0)))
+    d.add_sphere((0, 1, 0), 1.0, 0)
+    d.add_sphere((0, -1000.125, 0), 1000.0, 3)
+    d.add_sphere((2, 1, 0), 1.0, 1)
+    d.add_sphere((-2, 1, 0), 1.0, 2)
+    d.add_sphere((-2, 1, 0), -.99, 2)
+    s, m = d.arrays()
+    gs, gm = G.scene("simple")
+    assert s.tobytes() == gs.tobytes() and m.tobytes() == gm.tobytes()
+
+
+def test_save_ppm(tmp_path):
+    img = np.arange(2 * 3 * 3, dtype=np.uint8).reshape(2, 3, 3)
+    p = tmp_path / "x.ppm"
+    rt.save_ppm(str(p), img)
+    raw = p.read_bytes()
+    assert raw.startswith(b"P6\n3 2\n255\n") and raw[len(b"P6\n3 2\n255\n"):] == img.tobytes()

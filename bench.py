@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--camera", default="reference", choices=["reference", "corrected"])
-    ap.add_argument("--variant", default="lds", choices=["lds", "scalar"])
+    ap.add_argument("--variant", default="lds", choices=["lds", "scalar", "fast"])
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=32, help="rows in the CPU-baseline sample")
@@ -116,7 +116,7 @@ def main():
         raise SystemExit(f"height {H} is not divisible by {world} ranks")
     rows = H // world
     params = rt.make_params(W, H, spp, depth, args.seed, row_offset=rank, row_stride=world, num_rows=rows,
-                            scalar_scene=args.variant == "scalar")
+                            scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast")
     dev = torch.device("cuda", local)
     ds = rt.DeviceScene(arrays, device=local)
     tile = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
@@ -183,7 +183,7 @@ def main():
             "data": "synthetic (reference huge scene, std::mt19937 seed 1234; per-sample PCG32 seed %d)" % args.seed,
             "config": {"workload": WORKLOAD[args.config], "scene": f"{scene_name} ({n_spheres} spheres)",
                        "width": W, "height": H, "spp": spp, "max_depth": depth, "camera": args.camera,
-                       "kernel": f"exact-{args.variant}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
+                       "kernel": "fast-lds (FMA, tolerance)" if args.variant == "fast" else f"exact-{args.variant} (bit-exact)", "parallelism": f"row-interleaved x{world}, RCCL gather"},
             "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
             "segments_per_primary": round(segments_all / primaries, 4),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,

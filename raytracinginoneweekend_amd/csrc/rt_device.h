@@ -41,6 +41,7 @@ struct KParams {
     float *slots;            // [slot_end - slot_begin][n_pixels][3]
     uint32_t *queue_ctr;     // [8]
     unsigned long long *segments;  // optional
+    unsigned long long *dbg;       // [8] diagnostic counters (V_STATS_LDS only)
 };
 
 struct KAccum {
@@ -53,6 +54,6 @@ struct KAccum {
     uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame;
 };
 
-enum Variant : int { V_EXACT_LDS = 0, V_EXACT_SCALAR = 1, V_FAST_LDS = 2 };
+enum Variant : int { V_EXACT_LDS = 0, V_EXACT_SCALAR = 1, V_FAST_LDS = 2, V_STATS_LDS = 3 };
 
 } // namespace rt

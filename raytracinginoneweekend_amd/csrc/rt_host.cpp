@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -20,8 +21,8 @@
 #include "rt_device.h"
 
 namespace rt {
-hipError_t launch_render(int variant, const KParams &p, uint32_t grid, hipStream_t stream);
-hipError_t occupancy_render(int variant, int *blocks_per_cu, size_t lds);
+hipError_t launch_render(int variant, int block, const KParams &p, uint32_t grid, hipStream_t stream);
+hipError_t occupancy_render(int variant, int block, int *blocks_per_cu, size_t lds);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_t stream);
 } // namespace rt
@@ -72,7 +73,8 @@ struct rt_scene {
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;
     int cu_count = 0;
-    int occ_lds = -1, occ_scalar = -1;
+    int occ[4][9];  // [variant][block] blocks per CU, -1 = not queried
+    unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     size_t max_lds = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
     static constexpr uint32_t kRing = 256;
@@ -221,8 +223,24 @@ int check_params(const rt_params *p)
         return fail(RT_ERR_INVALID, "params: rows exceed the image height");
     if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE))
         return fail(RT_ERR_INVALID, "params: unknown flag");
-    if (p->flags & RT_FLAG_FAST_MATH) return fail(RT_ERR_UNSUPPORTED, "params: fast-math kernel not built yet");
     return RT_OK;
+}
+
+// Sphere block of the closest-hit loop (2, 4 or 8; default 8, measured fastest on MI355X);
+// RT_SPHERE_BLOCK overrides it
+// (a tuning knob for ablations; every block size gives identical bits).
+int kernel_block()
+{
+    const char *e = std::getenv("RT_SPHERE_BLOCK");
+    const int v = e ? std::atoi(e) : 8;
+    return (v == 2 || v == 4 || v == 8) ? v : 8;
+}
+
+// RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
+bool debug_stats()
+{
+    const char *e = std::getenv("RT_DEBUG_STATS");
+    return e && e[0] == '1';
 }
 
 int ensure(void **ptr, size_t *have, size_t want)
@@ -268,7 +286,7 @@ int rt_scene_destroy(rt_scene *sc)
     for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
     for (auto e : sc->ev_end) (void)hipEventDestroy(e);
     for (void *p : {(void *)sc->geo, (void *)sc->full, (void *)sc->mat_data, (void *)sc->sph_mat,
-                    (void *)sc->mat_kind, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
+                    (void *)sc->mat_kind, (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
     delete sc;
@@ -295,8 +313,8 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
 
     // Packed device layout: geo = {cx, cy, cz, fl(r*r)} padded to a multiple
     // of 4 with never-hit entries (r*r = -inf makes the discriminant -inf or NaN).
-    const uint32_t padded = (n_spheres + 3u) & ~3u;
-    std::vector<float> geo(static_cast<size_t>(std::max(padded, 4u)) * 4, 0.f), full(std::max(n_spheres, 1u) * 4, 0.f);
+    const uint32_t padded = (n_spheres + 7u) & ~7u;
+    std::vector<float> geo(static_cast<size_t>(std::max(padded, 8u)) * 4, 0.f), full(std::max(n_spheres, 1u) * 4, 0.f);
     std::vector<uint32_t> smat(std::max(n_spheres, 1u), 0u), kind(n_materials);
     std::vector<float> md(static_cast<size_t>(n_materials) * 4);
     for (uint32_t i = 0; i < padded; ++i) {
@@ -317,6 +335,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         md[4 * i + 3] = materials[i].param;
     }
     rt_scene *sc = new rt_scene();
+    for (auto &r : sc->occ) for (auto &x : r) x = -1;
     sc->device = device;
     sc->n_spheres = n_spheres;
     sc->n_padded = padded;
@@ -414,9 +433,19 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     int variant = (P.flags & RT_FLAG_SCALAR_SCENE) ? rt::V_EXACT_SCALAR : rt::V_EXACT_LDS;
     const size_t lds = static_cast<size_t>(sc->n_padded) * 16u;
     if (variant == rt::V_EXACT_LDS && lds > sc->max_lds) variant = rt::V_EXACT_SCALAR;
-    int &occ = variant == rt::V_EXACT_LDS ? sc->occ_lds : sc->occ_scalar;
+    if ((P.flags & RT_FLAG_FAST_MATH) && lds <= sc->max_lds) variant = rt::V_FAST_LDS;
+    if (variant == rt::V_EXACT_LDS && debug_stats()) {
+        variant = rt::V_STATS_LDS;
+        if (!sc->dbg) {
+            RT_HIP(hipMalloc((void **)&sc->dbg, 8 * sizeof(unsigned long long)));
+            RT_HIP(hipMemset(sc->dbg, 0, 8 * sizeof(unsigned long long)));
+        }
+        k.dbg = sc->dbg;
+    }
+    const int block = variant == rt::V_STATS_LDS ? 8 : kernel_block();
+    int &occ = sc->occ[variant][block];
     if (occ < 0) {
-        RT_HIP(rt::occupancy_render(variant, &occ, variant == rt::V_EXACT_LDS ? lds : 0));
+        RT_HIP(rt::occupancy_render(variant, block, &occ, variant == rt::V_EXACT_LDS ? lds : 0));
         occ = std::max(occ, 1);
     }
 
@@ -441,7 +470,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_chunks + 3u) / 4u)));
         RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * sizeof(uint32_t), st));
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
-        RT_HIP(rt::launch_render(variant, k, grid, st));
+        RT_HIP(rt::launch_render(variant, block, k, grid, st));
         if (s1 == k.n_slots) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
         rt::KAccum a{};
         a.slots = sc->slots;
@@ -476,6 +505,20 @@ int rt_scene_kernel_times(rt_scene *sc, uint32_t max, float *ms, uint32_t *n)
         RT_HIP(hipEventElapsedTime(ms + i, sc->ev_begin[r], sc->ev_end[r]));
     }
     *n = cnt;
+    return RT_OK;
+}
+
+int rt_scene_debug_counters(rt_scene *sc, uint64_t out[8], int reset)
+{
+    if (!sc || !out) return fail(RT_ERR_INVALID, "rt_scene_debug_counters: null argument");
+    RT_HIP(hipSetDevice(sc->device));
+    if (!sc->dbg) {
+        std::memset(out, 0, 8 * sizeof(uint64_t));
+        return RT_OK;
+    }
+    RT_HIP(hipDeviceSynchronize());
+    RT_HIP(hipMemcpy(out, sc->dbg, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (reset) RT_HIP(hipMemset(sc->dbg, 0, 8 * sizeof(uint64_t)));
     return RT_OK;
 }
 

@@ -121,56 +121,81 @@ __device__ __forceinline__ void pixel_of(const KParams &p, uint32_t i, uint32_t 
 // ---- closest hit over all spheres (raytracer.hxx:94-118) -----------------------------
 // Shrinking t_max with a strict '<' in index order == the reference's "all hits on
 // (kMIN, kMAX), then the first minimum" (near <= far, so a rejected near root never hides
-// an acceptable far root of the same sphere). Spheres come 4 at a time; the root work
-// (correctly rounded sqrt + two IEEE divides) runs only when some lane's discriminant is
-// positive for one of the 4.
-#define RT_TEST_DISC(k, S)                                                     \
-    const float ocx##k = o.x - S.x, ocy##k = o.y - S.y, ocz##k = o.z - S.z;    \
-    const float b##k = ocx##k * d.x + ocy##k * d.y + ocz##k * d.z;             \
-    const float c##k = ocx##k * ocx##k + ocy##k * ocy##k + ocz##k * ocz##k - S.w; \
-    const float disc##k = b##k * b##k - a * c##k;
-
-#define RT_ROOTS(k, idx)                                                       \
-    if (disc##k > 0.f) {                                                       \
-        const float q = sqrtf(disc##k);                                        \
-        float t = (-b##k - q) / a;                                             \
-        if (t < tb && t > RT_TMIN) { tb = t; ib = (idx); }                     \
-        else {                                                                 \
-            t = (-b##k + q) / a;                                               \
-            if (t < tb && t > RT_TMIN) { tb = t; ib = (idx); }                 \
-        }                                                                      \
-    }
-
-template <int V>
-__device__ __forceinline__ int closest_hit(const KParams &p, const float4 *__restrict__ geo, f3 o, f3 d, float &tb)
+// an acceptable far root of the same sphere).
+// Spheres come BLOCK at a time: the BLOCK discriminants are formed first, and the root work
+// (correctly rounded sqrt + IEEE divides) runs only when some lane's discriminant is positive
+// for one of them (tested as max3 of the discriminants: NaN never wins, NaN > 0 is false).
+// Diagnostic counters (STATS builds only; see rt_scene_debug_counters): per-lane tallies
+// plus wave-level ones counted by the first active lane.
+struct Dbg {
+    uint32_t wave_blocks, lane_blocks, wave_roots, lane_roots;
+};
+__device__ __forceinline__ bool first_active_lane()
 {
+    return (threadIdx.x & 63u) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63u);
+}
+
+template <int V, int BLOCK, bool STATS>
+__device__ __forceinline__ int closest_hit(const KParams &p, const float4 *__restrict__ geo, f3 o, f3 d, float &tb,
+                                           Dbg &dbg)
+{
+    constexpr bool FAST = (V == V_FAST_LDS);
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
+    const float inv_a = FAST ? __builtin_amdgcn_rcpf(a) : 0.f;
     tb = RT_TMAX;
     int ib = -1;
-    const uint32_t n = p.n_spheres_padded;  // multiple of 4; padding: rr = -inf never hits
-    for (uint32_t i = 0; i < n; i += 4) {
-        const float4 s0 = geo[i], s1 = geo[i + 1], s2 = geo[i + 2], s3 = geo[i + 3];
-        RT_TEST_DISC(0, s0)
-        RT_TEST_DISC(1, s1)
-        RT_TEST_DISC(2, s2)
-        RT_TEST_DISC(3, s3)
-        if ((disc0 > 0.f) | (disc1 > 0.f) | (disc2 > 0.f) | (disc3 > 0.f)) {
-            RT_ROOTS(0, (int)i)
-            RT_ROOTS(1, (int)i + 1)
-            RT_ROOTS(2, (int)i + 2)
-            RT_ROOTS(3, (int)i + 3)
+    const uint32_t n = p.n_spheres_padded;  // multiple of 8; padding: r*r = -inf never hits
+    for (uint32_t i = 0; i < n; i += BLOCK) {
+        float bq[BLOCK], dq[BLOCK];
+#pragma unroll
+        for (int k = 0; k < BLOCK; ++k) {
+            const float4 s = geo[i + k];
+            const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;   // raytracer.hxx:55
+            if (FAST) {  // contracted: 11 VALU per sphere
+                const float b = fmaf(ocx, d.x, fmaf(ocy, d.y, ocz * d.z));
+                const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -s.w)));
+                bq[k] = b;
+                dq[k] = fmaf(b, b, -(a * c));
+            } else {     // the reference's rounding, op by op: 17 VALU per sphere
+                const float b = ocx * d.x + ocy * d.y + ocz * d.z;           // :57
+                const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;     // :58
+                bq[k] = b;
+                dq[k] = b * b - a * c;                                       // :60
+            }
+        }
+        float m = dq[0];
+#pragma unroll
+        for (int k = 1; k < BLOCK; ++k) m = fmaxf(m, dq[k]);
+        if (m > 0.f) {
+            if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
+#pragma unroll
+            for (int k = 0; k < BLOCK; ++k) {
+                if (dq[k] > 0.f) {                                           // :62
+                    if (STATS) { ++dbg.lane_roots; if (first_active_lane()) ++dbg.wave_roots; }
+                    const float q = FAST ? __builtin_amdgcn_sqrtf(dq[k]) : sqrtf(dq[k]);
+                    float t = FAST ? (-bq[k] - q) * inv_a : (-bq[k] - q) / a;  // :63
+                    if (t < tb && t > RT_TMIN) { tb = t; ib = (int)(i + k); }
+                    else {
+                        t = FAST ? (q - bq[k]) * inv_a : (-bq[k] + q) / a;    // :76
+                        if (t < tb && t > RT_TMIN) { tb = t; ib = (int)(i + k); }
+                    }
+                }
+            }
         }
     }
     return ib;
 }
 
 // ---- the megakernel ----------------------------------------------------------------------
-template <int V>
-__global__ __launch_bounds__(256) void render_kernel(const KParams p)
+#ifndef RT_MIN_WAVES_PER_SIMD
+#define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
+#endif
+template <int V, int BLOCK, bool STATS>
+__global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(const KParams p)
 {
     extern __shared__ float4 lds_geo[];
     const float4 *geo;
-    if (V == V_EXACT_SCALAR) {
+    if constexpr (V == V_EXACT_SCALAR) {
         geo = reinterpret_cast<const float4 *>(p.sph_geo);
     } else {
         const float4 *src = reinterpret_cast<const float4 *>(p.sph_geo);
@@ -194,10 +219,13 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams p)
     uint32_t depth = 0;
     uint64_t rng = 0;
     unsigned long long segs = 0;
+    Dbg dbg{0, 0, 0, 0};
+    uint32_t dbg_iters = 0, dbg_refills = 0;
 
     for (;;) {
         // ---- refill items for idle lanes -------------------------------------------
         uint64_t need = __ballot(!has_item);
+        if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
             if (cnext >= cend) {
                 uint32_t c = 0;
@@ -257,6 +285,7 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams p)
             alive = true;
         }
         if (__ballot(alive) == 0) break;  // only when the item space is exhausted
+        if (STATS && lane == 0) ++dbg_iters;
 
         // ---- one segment for every live lane ------------------------------------------
         if (alive) {
@@ -267,7 +296,7 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams p)
             } else {
                 ++segs;
                 float t;
-                const int ib = closest_hit<V>(p, geo, o, d, t);
+                const int ib = closest_hit<V, BLOCK, STATS>(p, geo, o, d, t, dbg);
                 ++depth;
                 if (ib < 0) {
                     // main.cxx:71: background(.5 * unit_direction.y + 1) * attenuation
@@ -354,6 +383,16 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams p)
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0) atomicAdd(p.segments, v);
     }
+    if (STATS && p.dbg) {
+        const uint32_t c[7] = {dbg_iters, dbg_refills, dbg.wave_blocks, dbg.lane_blocks, dbg.wave_roots,
+                               dbg.lane_roots, (uint32_t)segs};
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            unsigned long long v = c[i];
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) atomicAdd(p.dbg + i, v);
+        }
+    }
 }
 
 // ---- ordered accumulation of the slots, average, optional gamma/u8 --------------------
@@ -411,32 +450,43 @@ __global__ __launch_bounds__(256) void epilogue_rgb8_kernel(const float *in, uin
 }
 
 // ---- launchers (called from rt_host.cpp) ---------------------------------------------
-hipError_t launch_render(int variant, const KParams &p, uint32_t grid, hipStream_t stream)
+// variant = scene source (V_EXACT_LDS / V_EXACT_SCALAR) x sphere block (2, 4, 8).
+template <int V, int B> static const void *kernel_ptr() { return reinterpret_cast<const void *>(&render_kernel<V, B, false>); }
+
+static const void *render_ptr(int variant, int block)
 {
-    const size_t lds = (variant == V_EXACT_SCALAR) ? 0 : (size_t)p.n_spheres_padded * 16u;
-    switch (variant) {
-    case V_EXACT_LDS:
-        hipLaunchKernelGGL(render_kernel<V_EXACT_LDS>, dim3(grid), dim3(256), lds, stream, p);
-        break;
-    case V_EXACT_SCALAR:
-        hipLaunchKernelGGL(render_kernel<V_EXACT_SCALAR>, dim3(grid), dim3(256), 0, stream, p);
-        break;
-    default:
-        return hipErrorInvalidValue;
+    if (variant == V_STATS_LDS) return reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, 8, true>);
+    if (variant == V_FAST_LDS) {
+        if (block == 2) return kernel_ptr<V_FAST_LDS, 2>();
+        if (block == 4) return kernel_ptr<V_FAST_LDS, 4>();
+        if (block == 8) return kernel_ptr<V_FAST_LDS, 8>();
     }
-    return hipGetLastError();
+    if (variant == V_EXACT_LDS) {
+        if (block == 2) return kernel_ptr<V_EXACT_LDS, 2>();
+        if (block == 4) return kernel_ptr<V_EXACT_LDS, 4>();
+        if (block == 8) return kernel_ptr<V_EXACT_LDS, 8>();
+    } else if (variant == V_EXACT_SCALAR) {
+        if (block == 2) return kernel_ptr<V_EXACT_SCALAR, 2>();
+        if (block == 4) return kernel_ptr<V_EXACT_SCALAR, 4>();
+        if (block == 8) return kernel_ptr<V_EXACT_SCALAR, 8>();
+    }
+    return nullptr;
 }
 
-hipError_t occupancy_render(int variant, int *blocks_per_cu, size_t lds)
+hipError_t launch_render(int variant, int block, const KParams &p, uint32_t grid, hipStream_t stream)
 {
-    switch (variant) {
-    case V_EXACT_LDS:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, render_kernel<V_EXACT_LDS>, 256, lds);
-    case V_EXACT_SCALAR:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, render_kernel<V_EXACT_SCALAR>, 256, 0);
-    default:
-        return hipErrorInvalidValue;
-    }
+    const void *fn = render_ptr(variant, block);
+    if (!fn) return hipErrorInvalidValue;
+    const size_t lds = (variant == V_EXACT_SCALAR) ? 0 : (size_t)p.n_spheres_padded * 16u;
+    void *args[] = {const_cast<KParams *>(&p)};
+    return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, stream);
+}
+
+hipError_t occupancy_render(int variant, int block, int *blocks_per_cu, size_t lds)
+{
+    const void *fn = render_ptr(variant, block);
+    if (!fn) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
 }
 
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream)

@@ -97,6 +97,13 @@ class DeviceScene:
         check(lib().rt_scene_kernel_times(self.handle, max_calls, buf, C.byref(n)))
         return list(buf[:n.value])
 
+    def debug_counters(self, reset=True):
+        """Counters of the instrumented kernel (RT_DEBUG_STATS=1), see rt_scene_debug_counters."""
+        buf = (C.c_uint64 * 8)()
+        check(lib().rt_scene_debug_counters(self.handle, buf, 1 if reset else 0))
+        keys = ["wave_iters", "wave_refills", "wave_blocks", "lane_blocks", "wave_roots", "lane_roots", "segments"]
+        return dict(zip(keys, list(buf)[:7]))
+
     def close(self):
         if self.handle:
             lib().rt_scene_destroy(self.handle)

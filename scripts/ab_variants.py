@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""A/B the render-kernel variants in ONE process, interleaved rounds (guide §5.4 rule 24).
+
+Every variant must produce bit-identical frames; prints per-variant median/min kernel ms.
+    python scripts/ab_variants.py [--config c3] [--rounds 5] [--variants lds:4,scalar:4,...]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+import raytracinginoneweekend_amd as rt  # noqa: E402
+from bench import CONFIGS  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c3")
+ap.add_argument("--camera", default="reference")
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--variants", default="lds:2,lds:4,lds:8,scalar:2,scalar:4,scalar:8")
+a = ap.parse_args()
+scene, W, H, spp, depth = CONFIGS[a.config]
+arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
+cam = rt.Camera.default(W, H, rt.CORRECTED if a.camera == "corrected" else rt.REFERENCE)
+ds = rt.DeviceScene(arrays)
+out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+seg = torch.zeros(1, dtype=torch.int64, device="cuda")
+stream = torch.cuda.current_stream().cuda_stream
+variants = [v.split(":") for v in a.variants.split(",")]
+times = {f"{k}:{b}": [] for k, b in variants}
+ref = None
+segs = {}
+for r in range(a.rounds + 1):
+    for kind, block in variants:
+        os.environ["RT_SPHERE_BLOCK"] = block
+        extra = {"fast_math": True} if kind.startswith("fast") else {}
+        p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind.endswith("scalar"), **extra)
+        seg.zero_()
+        ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr())
+        torch.cuda.synchronize()
+        ms = ds.kernel_times(1)[0]
+        name = f"{kind}:{block}"
+        if r == 0:  # warm-up round: check bits
+            img = out.cpu()
+            if ref is None:
+                ref = img
+            same = torch.equal(img.view(torch.int32), ref.view(torch.int32))
+            segs[name] = int(seg.item())
+            d = (img - ref).abs()
+            px = d.amax(dim=-1)
+            print(f"{name}: identical={same} segments={segs[name]} max|d|={d.max().item():.3g} "
+                  f"mean|d|={d.mean().item():.3g} px<=1e-4: {(px <= 1e-4).float().mean().item()*100:.3f}% "
+                  f"px<=1e-3: {(px <= 1e-3).float().mean().item()*100:.3f}%", flush=True)
+            if os.environ.get("RT_DEBUG_STATS") == "1":
+                print(f"{name}: counters {ds.debug_counters()}", flush=True)
+        else:
+            times[name].append(ms)
+res = {}
+for name, t in times.items():
+    prim = W * H * spp
+    res[name] = {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
+                 "mrays": round(prim / statistics.median(t) / 1e3, 1),
+                 "tflops": round(segs[name] * len(arrays[0]) * 20 / statistics.median(t) / 1e9, 2)}
+    print(name, json.dumps(res[name]), flush=True)

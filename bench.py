@@ -18,7 +18,6 @@ import json
 import os
 import subprocess
 import sys
-import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -112,27 +111,20 @@ def main():
     n_spheres = len(arrays[0])
     mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
     cam = rt.Camera.default(W, H, mode)
-    if H % world:
-        raise SystemExit(f"height {H} is not divisible by {world} ranks")
-    rows = H // world
-    params = rt.make_params(W, H, spp, depth, args.seed, row_offset=rank, row_stride=world, num_rows=rows,
-                            scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast")
+    from raytracinginoneweekend_amd.rowtiles import FrameGather, rank_params
+    params = rank_params(W, H, spp, world, rank, max_depth=depth, seed=args.seed,
+                         scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast")
+    rows = params.num_rows
     dev = torch.device("cuda", local)
     ds = rt.DeviceScene(arrays, device=local)
     tile = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
-    frame = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if rank == 0 else None
-    gather = [torch.empty_like(tile) for _ in range(world)] if (rank == 0 and distributed) else None
+    gather = FrameGather(tile, world, rank)
     seg = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     def step(count_segments):
         ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
-        if distributed:
-            dist.gather(tile, gather_list=gather, dst=0)
-            if rank == 0:
-                frame.view(rows, world, W, 3).copy_(torch.stack(gather, dim=1))
-        else:
-            frame.copy_(tile)
+        gather(tile)
 
     for _ in range(args.warmup):
         step(False)

@@ -25,6 +25,7 @@ sys.path.insert(0, REPO)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X f32 vector peak (MI355X_MICROARCH.md, chip-level table)
 FLOP_PER_TEST = 20         # one ray-sphere test, SURVEY.md §8(d): 17 to the discriminant + 3 root
+FLOP_PER_BOX = 19          # one padded cluster-AABB slab test
 CONFIGS = {
     # name: (scene, W, H, spp, depth)
     "c3": ("huge", 1280, 720, 128, 64),
@@ -49,7 +50,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--camera", default="reference", choices=["reference", "corrected"])
-    ap.add_argument("--variant", default="lds", choices=["lds", "scalar", "fast"])
+    ap.add_argument("--variant", default="exact", choices=["exact", "fast", "scalar"],
+                    help="exact: bit-exact kernel; fast: FMA kernel within the stated tolerance; "
+                         "scalar: brute-force scalar-cache A/B")
+    ap.add_argument("--traversal", default="cull", choices=["cull", "brute"],
+                    help="cull: exact cluster culling (same bits); brute: every sphere, as the reference")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=32, help="rows in the CPU-baseline sample")
@@ -113,13 +118,14 @@ def main():
     cam = rt.Camera.default(W, H, mode)
     from raytracinginoneweekend_amd.rowtiles import FrameGather, rank_params
     params = rank_params(W, H, spp, world, rank, max_depth=depth, seed=args.seed,
-                         scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast")
+                         scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast",
+                         brute_force=args.traversal == "brute")
     rows = params.num_rows
     dev = torch.device("cuda", local)
     ds = rt.DeviceScene(arrays, device=local)
     tile = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
     gather = FrameGather(tile, world, rank)
-    seg = torch.zeros(1, dtype=torch.int64, device=dev)
+    seg = torch.zeros(3, dtype=torch.int64, device=dev)  # segments, sphere tests, box tests
     stream = torch.cuda.current_stream(dev)
 
     def step(count_segments):
@@ -142,14 +148,14 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kt = ds.kernel_times(args.steps)  # render-kernel durations of the timed steps (HIP events)
-    segments = int(seg.item())
+    segments, sph_tests, box_tests = [int(x) for x in seg.tolist()]
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        sg = torch.tensor([segments], dtype=torch.int64, device=dev)
+        sg = seg.clone()
         dist.all_reduce(sg)
-        segments_all = int(sg.item())
+        segments_all = int(sg[0].item())
     else:
         segments_all = segments
 
@@ -157,8 +163,11 @@ def main():
     value = primaries / elapsed / 1e6
     # roofline of the dominant kernel (render_kernel) on this rank
     k_avg_ms = sum(kt) / len(kt)
-    flop_per_launch = segments / args.steps * n_spheres * FLOP_PER_TEST
+    # executed work: every ray-sphere test the kernel ran (20 FLOP) + every cluster AABB test
+    # (19 FLOP); brute force executes segments x n_spheres tests
+    flop_per_launch = (sph_tests * FLOP_PER_TEST + box_tests * FLOP_PER_BOX) / args.steps
     achieved = flop_per_launch / (k_avg_ms * 1e-3) / 1e12
+    brute_equiv = segments / args.steps * n_spheres * FLOP_PER_TEST / (k_avg_ms * 1e-3) / 1e12
     if rank == 0:
         rec = {
             "metric": "Mrays/sec + frame wall-clock, huge-scene 1280x720x128spp @1/2/4/8 GPU",
@@ -175,13 +184,17 @@ def main():
             "data": "synthetic (reference huge scene, std::mt19937 seed 1234; per-sample PCG32 seed %d)" % args.seed,
             "config": {"workload": WORKLOAD[args.config], "scene": f"{scene_name} ({n_spheres} spheres)",
                        "width": W, "height": H, "spp": spp, "max_depth": depth, "camera": args.camera,
-                       "kernel": "fast-lds (FMA, tolerance)" if args.variant == "fast" else f"exact-{args.variant} (bit-exact)", "parallelism": f"row-interleaved x{world}, RCCL gather"},
+                       "kernel": ("fast (FMA, stated tolerance)" if args.variant == "fast" else f"{args.variant} (bit-exact)")
+                       + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
             "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
             "segments_per_primary": round(segments_all / primaries, 4),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
                          "kernel": "render_kernel", "kernel_avg_ms": round(k_avg_ms, 3),
-                         "flop_per_launch": flop_per_launch},
+                         "flop_per_launch": flop_per_launch, "work": "executed sphere+box tests",
+                         "brute_force_equiv_tflops": round(brute_equiv, 2)},
+            "tests_per_segment": round(sph_tests / max(segments, 1), 2),
+            "boxes_per_segment": round(box_tests / max(segments, 1), 2),
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], args.camera, args.seed, args.cpu_rows,

@@ -93,7 +93,8 @@ typedef struct rt_camera {
 enum rt_flags {
     RT_FLAG_FULL_FRAME = 1u << 0, /* write rows at their global position             */
     RT_FLAG_FAST_MATH = 1u << 1,  /* FMA-contracted kernel, stated tolerance          */
-    RT_FLAG_SCALAR_SCENE = 1u << 2 /* read spheres via the scalar cache, not LDS       */
+    RT_FLAG_SCALAR_SCENE = 1u << 2, /* A/B: brute force, spheres via the scalar cache   */
+    RT_FLAG_BRUTE_FORCE = 1u << 3   /* test every sphere (no cluster culling); same bits */
 };
 typedef struct rt_params {
     uint32_t width, height;
@@ -106,7 +107,8 @@ typedef struct rt_params {
 typedef struct rt_stats {
     uint64_t primaries;  /* pixel-samples traced (W*rows*spp)                          */
     uint64_t segments;   /* hit_world() calls = ray segments traced                    */
-    uint64_t sphere_tests; /* segments * n_spheres                                     */
+    uint64_t sphere_tests; /* ray-sphere tests executed (lane level)                   */
+    uint64_t box_tests;  /* cluster AABB tests executed (lane level)                    */
     double kernel_ms;    /* render kernel time (HIP events)                            */
     double wall_ms;      /* whole call: upload + kernel + download                     */
 } rt_stats;
@@ -161,8 +163,9 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres,
                     rt_scene **out);
 int rt_scene_destroy(rt_scene *scene);
 /* Enqueue one render on `stream` (a hipStream_t, or NULL for the null stream).
- * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64
- * that receives the segment count (accumulated; zero it first). No host sync.        */
+ * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64[3]
+ * that accumulates {segments, sphere tests, cluster box tests} (zero it first). No
+ * host sync.                                                                          */
 int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
                      float *d_rgb, void *stream, uint64_t *d_segments);
 /* Durations (ms, HIP events on the render stream) of the render kernel launches of the

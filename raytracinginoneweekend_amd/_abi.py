@@ -20,6 +20,7 @@ RT_CAMERA_REFERENCE, RT_CAMERA_CORRECTED = 0, 1
 RT_FLAG_FULL_FRAME = 1 << 0
 RT_FLAG_FAST_MATH = 1 << 1
 RT_FLAG_SCALAR_SCENE = 1 << 2
+RT_FLAG_BRUTE_FORCE = 1 << 3
 
 
 class RtSphere(C.Structure):
@@ -54,6 +55,7 @@ class RtParams(C.Structure):
 class RtStats(C.Structure):
     _fields_ = [
         ("primaries", C.c_uint64), ("segments", C.c_uint64), ("sphere_tests", C.c_uint64),
+        ("box_tests", C.c_uint64),
         ("kernel_ms", C.c_double), ("wall_ms", C.c_double),
     ]
 

@@ -1,6 +1,7 @@
 // rt_device.h — parameters shared by the host launcher (rt_host.cpp) and the HIP kernels
-// (rt_kernel.hip). Plain C++ POD; no HIP types, so both sides include it.
+// (rt_kernel.hip). Plain POD records (HIP vector types only), included by both sides.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace rt {
@@ -31,8 +32,14 @@ struct KParams {
     uint32_t slot_begin, slot_end;          // this launch's slots
     uint32_t n_items, n_chunks;
     // scene
-    uint32_t n_spheres, n_spheres_padded, n_materials;
-    const float *sph_geo;    // [n_spheres_padded][4] = cx, cy, cz, fl(r*r); padding never hits
+    uint32_t n_spheres, n_materials;
+    // scene blob, staged whole into LDS: [geo: n_geo float4 {cx, cy, cz, fl(r*r)}]
+    // [sidx: n_geo u32 original indices, padded to 16 B][clusters: n_clusters x 2 float4].
+    // geo = the always-tested list (n_always, multiple of 8) then each cluster's members
+    // (padded to 8); padding entries have r*r = -inf and never hit.
+    const float4 *blob;
+    uint32_t blob_units;     // 16-byte units
+    uint32_t n_geo, n_always, n_clusters, clus_offset;
     const float *sph_full;   // [n_spheres][4] = cx, cy, cz, r
     const uint32_t *sph_mat; // [n_spheres]
     const float *mat_data;   // [n_materials][4] = albedo rgb, param
@@ -40,7 +47,7 @@ struct KParams {
     // outputs / workspace
     float *slots;            // [slot_end - slot_begin][n_pixels][3]
     uint32_t *queue_ctr;     // [8]
-    unsigned long long *segments;  // optional
+    unsigned long long *segments;  // optional [3]: segments, sphere tests, cluster box tests
     unsigned long long *dbg;       // [8] diagnostic counters (V_STATS_LDS only)
 };
 

@@ -21,8 +21,8 @@
 #include "rt_device.h"
 
 namespace rt {
-hipError_t launch_render(int variant, int block, const KParams &p, uint32_t grid, hipStream_t stream);
-hipError_t occupancy_render(int variant, int block, int *blocks_per_cu, size_t lds);
+hipError_t launch_render(int variant, bool cull, const KParams &p, uint32_t grid, hipStream_t stream);
+hipError_t occupancy_render(int variant, bool cull, int *blocks_per_cu, size_t lds);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_t stream);
 } // namespace rt
@@ -63,8 +63,13 @@ constexpr uint32_t kMaxSlotsBytes = 1u << 31;  // slot workspace per pass (2 GiB
 
 struct rt_scene {
     int device = 0;
-    uint32_t n_spheres = 0, n_padded = 0, n_materials = 0;
-    float *geo = nullptr, *full = nullptr, *mat_data = nullptr;
+    uint32_t n_spheres = 0, n_materials = 0;
+    float *full = nullptr, *mat_data = nullptr;
+    // scene blobs: [0] every sphere in index order (brute force), [1] big
+    // spheres always tested + spatial clusters
+    float *blob[2] = {nullptr, nullptr};
+    uint32_t blob_units[2] = {0, 0}, n_geo[2] = {0, 0}, n_always[2] = {0, 0}, n_clusters[2] = {0, 0},
+             clus_offset[2] = {0, 0};
     uint32_t *sph_mat = nullptr, *mat_kind = nullptr;
     // workspace
     float *slots = nullptr;
@@ -73,7 +78,7 @@ struct rt_scene {
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;
     int cu_count = 0;
-    int occ[4][9];  // [variant][block] blocks per CU, -1 = not queried
+    int occ[4][2];  // [variant][cull] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     size_t max_lds = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
@@ -206,6 +211,118 @@ struct scene_builder {
     }
 };
 
+// ---- scene blob: always-tested list + spatial clusters -------------------
+struct blob_t {
+    std::vector<float> data;  // 16-byte units
+    uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0;
+};
+
+constexpr float kPadRel = 1e-3f;      // must match RT_PAD_REL in rt_kernel.hip
+constexpr uint32_t kClusterMax = 16;  // spheres per cluster (two blocks of 8)
+
+void split_clusters(const rt_sphere *s, std::vector<uint32_t> ids, std::vector<std::vector<uint32_t>> &out)
+{
+    if (ids.size() <= kClusterMax) {
+        out.push_back(std::move(ids));
+        return;
+    }
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i : ids)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], s[i].center[a]);
+            hi[a] = std::max(hi[a], s[i].center[a]);
+        }
+    int ax = 0;
+    for (int a = 1; a < 3; ++a)
+        if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+    // split at a multiple of the cluster size so leaves come out full
+    const size_t half = ((ids.size() / 2 + kClusterMax - 1) / kClusterMax) * kClusterMax;
+    const size_t mid = std::min(half, ids.size() - 1);
+    std::nth_element(ids.begin(), ids.begin() + mid, ids.end(), [&](uint32_t x, uint32_t y) {
+        return s[x].center[ax] < s[y].center[ax] || (s[x].center[ax] == s[y].center[ax] && x < y);
+    });
+    std::vector<uint32_t> left(ids.begin(), ids.begin() + mid), right(ids.begin() + mid, ids.end());
+    split_clusters(s, std::move(left), out);
+    split_clusters(s, std::move(right), out);
+}
+
+blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
+{
+    std::vector<uint32_t> always, rest;
+    if (clustered && n >= 2 * kClusterMax) {
+        std::vector<float> r(n);
+        for (uint32_t i = 0; i < n; ++i) r[i] = std::fabs(s[i].radius);
+        std::vector<float> sorted = r;
+        std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
+        const float big = 4.f * sorted[n / 2];
+        for (uint32_t i = 0; i < n; ++i) {
+            const bool finite = std::isfinite(s[i].center[0]) && std::isfinite(s[i].center[1]) &&
+                                std::isfinite(s[i].center[2]) && std::isfinite(r[i]);
+            (finite && r[i] <= big ? rest : always).push_back(i);
+        }
+    } else {
+        for (uint32_t i = 0; i < n; ++i) always.push_back(i);
+    }
+    std::vector<std::vector<uint32_t>> clusters;
+    if (!rest.empty()) split_clusters(s, rest, clusters);
+    std::sort(clusters.begin(), clusters.end(), [](const auto &x, const auto &y) { return x.front() < y.front(); });
+
+    auto pad8 = [](uint32_t x) { return (x + 7u) & ~7u; };
+    std::vector<float> geo;
+    std::vector<uint32_t> sidx;
+    auto push = [&](const std::vector<uint32_t> &ids) {
+        const uint32_t base = static_cast<uint32_t>(sidx.size());
+        for (uint32_t i : ids) {
+            geo.insert(geo.end(), {s[i].center[0], s[i].center[1], s[i].center[2], s[i].radius * s[i].radius}); // raytracer.hxx:58
+            sidx.push_back(i);
+        }
+        while (sidx.size() < base + pad8(static_cast<uint32_t>(ids.size()))) {
+            geo.insert(geo.end(), {0.f, 0.f, 0.f, -INFINITY});  // never hits
+            sidx.push_back(0xffffffffu);
+        }
+        return base;
+    };
+    blob_t b;
+    push(always);
+    b.n_always = static_cast<uint32_t>(sidx.size());
+    std::vector<float> crec;
+    for (const auto &c : clusters) {
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i : c)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], s[i].center[a] - std::fabs(s[i].radius));
+                hi[a] = std::max(hi[a], s[i].center[a] + std::fabs(s[i].radius));
+            }
+        float C[3], E[3];
+        for (int a = 0; a < 3; ++a) {
+            C[a] = .5f * (lo[a] + hi[a]);
+            E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
+        }
+        const float kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
+        const uint32_t start = push(c);
+        const uint32_t cnt = pad8(static_cast<uint32_t>(c.size()));
+        uint32_t packed = start | (cnt << 16);
+        float pf;
+        std::memcpy(&pf, &packed, 4);
+        crec.insert(crec.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
+    }
+    b.n_geo = static_cast<uint32_t>(sidx.size());
+    b.n_clusters = static_cast<uint32_t>(clusters.size());
+    // layout in 16-byte units: geo | sidx (padded) | clusters
+    b.data = geo;
+    if (b.data.empty()) b.data.assign(4, 0.f);
+    std::vector<uint32_t> sp = sidx;
+    while (sp.size() % 4) sp.push_back(0xffffffffu);
+    for (uint32_t v : sp) {
+        float f;
+        std::memcpy(&f, &v, 4);
+        b.data.push_back(f);
+    }
+    b.clus_offset = static_cast<uint32_t>(b.data.size() / 4);
+    b.data.insert(b.data.end(), crec.begin(), crec.end());
+    return b;
+}
+
 uint32_t rows_of(const rt_params &p)
 {
     if (p.num_rows) return p.num_rows;
@@ -221,19 +338,9 @@ int check_params(const rt_params *p)
     const uint32_t rows = rows_of(*p);
     if (rows && static_cast<uint64_t>(p->row_offset) + static_cast<uint64_t>(rows - 1) * st >= p->height)
         return fail(RT_ERR_INVALID, "params: rows exceed the image height");
-    if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE))
+    if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE | RT_FLAG_BRUTE_FORCE))
         return fail(RT_ERR_INVALID, "params: unknown flag");
     return RT_OK;
-}
-
-// Sphere block of the closest-hit loop (2, 4 or 8; default 8, measured fastest on MI355X);
-// RT_SPHERE_BLOCK overrides it
-// (a tuning knob for ablations; every block size gives identical bits).
-int kernel_block()
-{
-    const char *e = std::getenv("RT_SPHERE_BLOCK");
-    const int v = e ? std::atoi(e) : 8;
-    return (v == 2 || v == 4 || v == 8) ? v : 8;
 }
 
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
@@ -285,7 +392,7 @@ int rt_scene_destroy(rt_scene *sc)
     (void)hipSetDevice(sc->device);
     for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
     for (auto e : sc->ev_end) (void)hipEventDestroy(e);
-    for (void *p : {(void *)sc->geo, (void *)sc->full, (void *)sc->mat_data, (void *)sc->sph_mat,
+    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->full, (void *)sc->mat_data, (void *)sc->sph_mat,
                     (void *)sc->mat_kind, (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
@@ -311,24 +418,16 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "rt_scene_create: bad device index");
     RT_HIP(hipSetDevice(device));
 
-    // Packed device layout: geo = {cx, cy, cz, fl(r*r)} padded to a multiple
-    // of 4 with never-hit entries (r*r = -inf makes the discriminant -inf or NaN).
-    const uint32_t padded = (n_spheres + 7u) & ~7u;
-    std::vector<float> geo(static_cast<size_t>(std::max(padded, 8u)) * 4, 0.f), full(std::max(n_spheres, 1u) * 4, 0.f);
+    std::vector<float> full(std::max(n_spheres, 1u) * 4, 0.f);
     std::vector<uint32_t> smat(std::max(n_spheres, 1u), 0u), kind(n_materials);
     std::vector<float> md(static_cast<size_t>(n_materials) * 4);
-    for (uint32_t i = 0; i < padded; ++i) {
-        if (i < n_spheres) {
-            const rt_sphere &s = spheres[i];
-            geo[4 * i] = s.center[0]; geo[4 * i + 1] = s.center[1]; geo[4 * i + 2] = s.center[2];
-            geo[4 * i + 3] = s.radius * s.radius;  // raytracer.hxx:58
-            full[4 * i] = s.center[0]; full[4 * i + 1] = s.center[1]; full[4 * i + 2] = s.center[2];
-            full[4 * i + 3] = s.radius;
-            smat[i] = s.material;
-        } else {
-            geo[4 * i + 3] = -INFINITY;
-        }
+    for (uint32_t i = 0; i < n_spheres; ++i) {
+        const rt_sphere &sp = spheres[i];
+        full[4 * i] = sp.center[0]; full[4 * i + 1] = sp.center[1]; full[4 * i + 2] = sp.center[2];
+        full[4 * i + 3] = sp.radius;
+        smat[i] = sp.material;
     }
+    blob_t blobs[2] = {build_blob(spheres, n_spheres, false), build_blob(spheres, n_spheres, true)};
     for (uint32_t i = 0; i < n_materials; ++i) {
         kind[i] = materials[i].kind;
         md[4 * i] = materials[i].albedo[0]; md[4 * i + 1] = materials[i].albedo[1]; md[4 * i + 2] = materials[i].albedo[2];
@@ -338,7 +437,6 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     for (auto &r : sc->occ) for (auto &x : r) x = -1;
     sc->device = device;
     sc->n_spheres = n_spheres;
-    sc->n_padded = padded;
     sc->n_materials = n_materials;
     auto up = [&](void **dst, const void *src, size_t bytes) -> int {
         RT_HIP(hipMalloc(dst, bytes));
@@ -346,7 +444,14 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         return RT_OK;
     };
     int rc = RT_OK;
-    if (rc == RT_OK) rc = up((void **)&sc->geo, geo.data(), geo.size() * 4);
+    for (int b = 0; b < 2 && rc == RT_OK; ++b) {
+        rc = up((void **)&sc->blob[b], blobs[b].data.data(), blobs[b].data.size() * 4);
+        sc->blob_units[b] = static_cast<uint32_t>(blobs[b].data.size() / 4);
+        sc->n_geo[b] = blobs[b].n_geo;
+        sc->n_always[b] = blobs[b].n_always;
+        sc->n_clusters[b] = blobs[b].n_clusters;
+        sc->clus_offset[b] = blobs[b].clus_offset;
+    }
     if (rc == RT_OK) rc = up((void **)&sc->full, full.data(), full.size() * 4);
     if (rc == RT_OK) rc = up((void **)&sc->sph_mat, smat.data(), smat.size() * 4);
     if (rc == RT_OK) rc = up((void **)&sc->mat_data, md.data(), md.size() * 4);
@@ -420,9 +525,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.g4 = P.spp / 4u;
     k.n_slots = k.g4 + P.spp % 4u;
     k.n_spheres = sc->n_spheres;
-    k.n_spheres_padded = sc->n_padded;
     k.n_materials = sc->n_materials;
-    k.sph_geo = sc->geo;
     k.sph_full = sc->full;
     k.sph_mat = sc->sph_mat;
     k.mat_data = sc->mat_data;
@@ -430,10 +533,15 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.queue_ctr = sc->queue_ctr;
     k.segments = reinterpret_cast<unsigned long long *>(d_segments);
 
-    int variant = (P.flags & RT_FLAG_SCALAR_SCENE) ? rt::V_EXACT_SCALAR : rt::V_EXACT_LDS;
-    const size_t lds = static_cast<size_t>(sc->n_padded) * 16u;
-    if (variant == rt::V_EXACT_LDS && lds > sc->max_lds) variant = rt::V_EXACT_SCALAR;
-    if ((P.flags & RT_FLAG_FAST_MATH) && lds <= sc->max_lds) variant = rt::V_FAST_LDS;
+    // Variant: exact (bit-exact) or fast (tolerance); clustered culling unless brute force is
+    // asked for; the scalar-cache A/B variant is brute force only. Each needs its blob in LDS.
+    int variant = (P.flags & RT_FLAG_FAST_MATH) ? rt::V_FAST_LDS : rt::V_EXACT_LDS;
+    bool cull = !(P.flags & RT_FLAG_BRUTE_FORCE) && sc->n_clusters[1] > 0;
+    if (P.flags & RT_FLAG_SCALAR_SCENE) { variant = rt::V_EXACT_SCALAR; cull = false; }
+    if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->blob_units[cull]) * 16u > sc->max_lds) {
+        if (variant == rt::V_FAST_LDS || cull) return fail(RT_ERR_UNSUPPORTED, "rt_render_device: scene too large for LDS");
+        variant = rt::V_EXACT_SCALAR;
+    }
     if (variant == rt::V_EXACT_LDS && debug_stats()) {
         variant = rt::V_STATS_LDS;
         if (!sc->dbg) {
@@ -442,10 +550,17 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         }
         k.dbg = sc->dbg;
     }
-    const int block = variant == rt::V_STATS_LDS ? 8 : kernel_block();
-    int &occ = sc->occ[variant][block];
+    const int b = cull ? 1 : 0;
+    k.blob = reinterpret_cast<const float4 *>(sc->blob[b]);
+    k.blob_units = sc->blob_units[b];
+    k.n_geo = sc->n_geo[b];
+    k.n_always = sc->n_always[b];
+    k.n_clusters = sc->n_clusters[b];
+    k.clus_offset = sc->clus_offset[b];
+    const size_t lds = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(k.blob_units) * 16u;
+    int &occ = sc->occ[variant][b];
     if (occ < 0) {
-        RT_HIP(rt::occupancy_render(variant, block, &occ, variant == rt::V_EXACT_LDS ? lds : 0));
+        RT_HIP(rt::occupancy_render(variant, cull, &occ, lds));
         occ = std::max(occ, 1);
     }
 
@@ -470,7 +585,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_chunks + 3u) / 4u)));
         RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * sizeof(uint32_t), st));
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
-        RT_HIP(rt::launch_render(variant, block, k, grid, st));
+        RT_HIP(rt::launch_render(variant, cull, k, grid, st));
         if (s1 == k.n_slots) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
         rt::KAccum a{};
         a.slots = sc->slots;
@@ -558,9 +673,9 @@ int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material 
         return rc == RT_OK;
     };
     if (chk(hipMalloc((void **)&d_rgb, n_values * 4), "hipMalloc") && u8_out) chk(hipMalloc((void **)&d_u8, n_values), "hipMalloc");
-    if (rc == RT_OK) chk(hipMalloc((void **)&d_seg, 8), "hipMalloc");
+    if (rc == RT_OK) chk(hipMalloc((void **)&d_seg, 24), "hipMalloc");
     if (rc == RT_OK && (P.flags & RT_FLAG_FULL_FRAME)) chk(hipMemset(d_rgb, 0, n_values * 4), "hipMemset");
-    if (rc == RT_OK) chk(hipMemset(d_seg, 0, 8), "hipMemset");
+    if (rc == RT_OK) chk(hipMemset(d_seg, 0, 24), "hipMemset");
     if (rc == RT_OK) chk(hipEventCreate(&e0), "hipEventCreate");
     if (rc == RT_OK) chk(hipEventCreate(&e1), "hipEventCreate");
     if (rc == RT_OK) chk(hipEventRecord(e0, nullptr), "hipEventRecord");
@@ -568,11 +683,11 @@ int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material 
     if (rc == RT_OK) chk(hipEventRecord(e1, nullptr), "hipEventRecord");
     if (rc == RT_OK && u8_out) rc = rt_epilogue_rgb8_device(d_rgb, d_u8, n_values / 3, nullptr);
     if (rc == RT_OK) chk(hipDeviceSynchronize(), "render");
-    uint64_t segs = 0;
+    uint64_t segs[3] = {0, 0, 0};
     float ms = 0.f;
     if (rc == RT_OK && rgb_out) chk(hipMemcpy(rgb_out, d_rgb, n_values * 4, hipMemcpyDeviceToHost), "hipMemcpy");
     if (rc == RT_OK && u8_out) chk(hipMemcpy(u8_out, d_u8, n_values, hipMemcpyDeviceToHost), "hipMemcpy");
-    if (rc == RT_OK) chk(hipMemcpy(&segs, d_seg, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == RT_OK) chk(hipMemcpy(segs, d_seg, 24, hipMemcpyDeviceToHost), "hipMemcpy");
     if (rc == RT_OK) chk(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -582,8 +697,9 @@ int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material 
     rt_scene_destroy(sc);
     if (rc == RT_OK && stats) {
         stats->primaries = static_cast<uint64_t>(P.width) * rows_of(P) * P.spp;
-        stats->segments = segs;
-        stats->sphere_tests = segs * n_spheres;
+        stats->segments = segs[0];
+        stats->sphere_tests = segs[1];
+        stats->box_tests = segs[2];
         stats->kernel_ms = ms;
         stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }

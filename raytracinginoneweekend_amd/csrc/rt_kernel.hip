@@ -118,13 +118,14 @@ __device__ __forceinline__ void pixel_of(const KParams &p, uint32_t i, uint32_t 
     }
 }
 
-// ---- closest hit over all spheres (raytracer.hxx:94-118) -----------------------------
-// Shrinking t_max with a strict '<' in index order == the reference's "all hits on
-// (kMIN, kMAX), then the first minimum" (near <= far, so a rejected near root never hides
-// an acceptable far root of the same sphere).
-// Spheres come BLOCK at a time: the BLOCK discriminants are formed first, and the root work
-// (correctly rounded sqrt + IEEE divides) runs only when some lane's discriminant is positive
-// for one of them (tested as max3 of the discriminants: NaN never wins, NaN > 0 is false).
+// ---- closest hit (raytracer.hxx:94-118) -------------------------------------------------
+// The reference tests every sphere on (kMIN, kMAX) and keeps the first minimum in index
+// order (stable_partition + min_element with a strict '<'). Here every sphere that is
+// tested yields the reference's per-sphere candidate (near root if in range, else far root,
+// raytracer.hxx:62-90) and candidates are compared on (t, original index) lexicographically
+// — the same minimum whatever order spheres are visited in, so the scene may be reordered
+// into spatial clusters. Spheres come 8 at a time: 8 discriminants, one
+// max reduction (NaN never wins) and the root work only when some lane needs it.
 // Diagnostic counters (STATS builds only; see rt_scene_debug_counters): per-lane tallies
 // plus wave-level ones counted by the first active lane.
 struct Dbg {
@@ -135,74 +136,116 @@ __device__ __forceinline__ bool first_active_lane()
     return (threadIdx.x & 63u) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63u);
 }
 
-template <int V, int BLOCK, bool STATS>
-__device__ __forceinline__ int closest_hit(const KParams &p, const float4 *__restrict__ geo, f3 o, f3 d, float &tb,
-                                           Dbg &dbg)
+struct Hit {
+    float t;
+    uint32_t id;   // original sphere index, 0xffffffff = none
+};
+
+template <bool FAST, bool STATS>
+__device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx, uint32_t i,
+                                            f3 o, f3 d, float a, Hit &h, Dbg &dbg)
 {
-    constexpr bool FAST = (V == V_FAST_LDS);
-    const float a = d.x * d.x + d.y * d.y + d.z * d.z;
-    const float inv_a = FAST ? __builtin_amdgcn_rcpf(a) : 0.f;
-    tb = RT_TMAX;
-    int ib = -1;
-    const uint32_t n = p.n_spheres_padded;  // multiple of 8; padding: r*r = -inf never hits
-    for (uint32_t i = 0; i < n; i += BLOCK) {
-        float bq[BLOCK], dq[BLOCK];
+    float bq[8], dq[8];
 #pragma unroll
-        for (int k = 0; k < BLOCK; ++k) {
-            const float4 s = geo[i + k];
-            const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;   // raytracer.hxx:55
-            if (FAST) {  // contracted: 11 VALU per sphere
-                const float b = fmaf(ocx, d.x, fmaf(ocy, d.y, ocz * d.z));
-                const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -s.w)));
-                bq[k] = b;
-                dq[k] = fmaf(b, b, -(a * c));
-            } else {     // the reference's rounding, op by op: 17 VALU per sphere
-                const float b = ocx * d.x + ocy * d.y + ocz * d.z;           // :57
-                const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;     // :58
-                bq[k] = b;
-                dq[k] = b * b - a * c;                                       // :60
-            }
+    for (int k = 0; k < 8; ++k) {
+        const float4 s = geo[i + k];
+        const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;       // raytracer.hxx:55
+        if (FAST) {  // contracted: 11 VALU per sphere
+            const float b = fmaf(ocx, d.x, fmaf(ocy, d.y, ocz * d.z));
+            const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -s.w)));
+            bq[k] = b;
+            dq[k] = fmaf(b, b, -(a * c));
+        } else {     // the reference's rounding, op by op: 17 VALU per sphere
+            const float b = ocx * d.x + ocy * d.y + ocz * d.z;               // :57
+            const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;         // :58
+            bq[k] = b;
+            dq[k] = b * b - a * c;                                           // :60
         }
-        float m = dq[0];
+    }
+    float m = fmaxf(fmaxf(fmaxf(dq[0], dq[1]), fmaxf(dq[2], dq[3])), fmaxf(fmaxf(dq[4], dq[5]), fmaxf(dq[6], dq[7])));
+    if (m > 0.f) {
+        if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
 #pragma unroll
-        for (int k = 1; k < BLOCK; ++k) m = fmaxf(m, dq[k]);
-        if (m > 0.f) {
-            if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
-#pragma unroll
-            for (int k = 0; k < BLOCK; ++k) {
-                if (dq[k] > 0.f) {                                           // :62
-                    if (STATS) { ++dbg.lane_roots; if (first_active_lane()) ++dbg.wave_roots; }
-                    const float q = FAST ? __builtin_amdgcn_sqrtf(dq[k]) : sqrtf(dq[k]);
-                    float t = FAST ? (-bq[k] - q) * inv_a : (-bq[k] - q) / a;  // :63
-                    if (t < tb && t > RT_TMIN) { tb = t; ib = (int)(i + k); }
-                    else {
-                        t = FAST ? (q - bq[k]) * inv_a : (-bq[k] + q) / a;    // :76
-                        if (t < tb && t > RT_TMIN) { tb = t; ib = (int)(i + k); }
-                    }
+        for (int k = 0; k < 8; ++k) {
+            if (dq[k] > 0.f) {                                               // :62
+                if (STATS) { ++dbg.lane_roots; if (first_active_lane()) ++dbg.wave_roots; }
+                const float q = sqrtf(dq[k]);
+                float t = (-bq[k] - q) / a;                                  // :63
+                if (!(t < RT_TMAX && t > RT_TMIN)) {
+                    t = (-bq[k] + q) / a;                                    // :76
+                    if (!(t < RT_TMAX && t > RT_TMIN)) t = __builtin_nanf("");
                 }
+                const uint32_t id = sidx[i + k];
+                if (t < h.t || (t == h.t && id < h.id)) { h.t = t; h.id = id; }
             }
         }
     }
-    return ib;
+}
+
+// Cluster culling: a lane tests a cluster's spheres only if its ray segment (kMIN, t_best]
+// can reach the cluster's AABB grown by a pad that dominates every float error involved
+// (1e-3 x (|o|_1 + |C|_1 + |e|_1) against errors below 3e-4 of that), so a
+// culled cluster never holds a sphere whose exact candidate could win: same bits.
+#define RT_PAD_REL 1e-3f
+
+template <bool FAST, bool CULL, bool STATS>
+__device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
+                                           const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
+                                           f3 d, Dbg &dbg, uint32_t &tests)
+{
+    const float a = d.x * d.x + d.y * d.y + d.z * d.z;
+    Hit h{RT_TMAX, 0xffffffffu};
+    for (uint32_t i = 0; i < p.n_always; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+    tests += p.n_always;
+    if (CULL) {
+        auto safe_rcp = [](float x) {
+            return __builtin_amdgcn_rcpf(fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x);
+        };
+        const float ix = safe_rcp(d.x), iy = safe_rcp(d.y), iz = safe_rcp(d.z);
+        const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
+        const float aix = fabsf(ix), aiy = fabsf(iy), aiz = fabsf(iz);
+        const float opad = RT_PAD_REL * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z));
+        for (uint32_t c = 0; c < p.n_clusters; ++c) {
+            const float4 c0 = clus[2 * c], c1 = clus[2 * c + 1];   // {C, ex}, {ey, ez, kc, start|count}
+            const float pad = opad + c1.z;
+            const float hx = (c0.w + pad) * aix, hy = (c1.x + pad) * aiy, hz = (c1.y + pad) * aiz;
+            const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
+            const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+            const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+            ++tests;  // box tests are tallied in the high half (see below)
+            if (tin <= tout && tout >= 0.5f * RT_TMIN && tin <= h.t * 1.002f) {
+                const uint32_t sc = __builtin_amdgcn_readfirstlane(__float_as_uint(c1.w));
+                const uint32_t start = sc & 0xffffu, cnt = sc >> 16;
+                for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                tests += cnt << 16;
+            }
+        }
+    }
+    return h;
 }
 
 // ---- the megakernel ----------------------------------------------------------------------
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
 #endif
-template <int V, int BLOCK, bool STATS>
+template <int V, bool CULL, bool STATS>
 __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(const KParams p)
 {
-    extern __shared__ float4 lds_geo[];
-    const float4 *geo;
+    constexpr bool FAST = (V == V_FAST_LDS);
+    // Scene blob -> LDS (or read in place from global for the scalar-cache A/B variant):
+    // [geo float4 x n_geo][sidx u32 x n_geo, 16-B padded][clusters float4 x 2 x n_clusters]
+    extern __shared__ float4 lds_blob[];
+    const float4 *blob;
     if constexpr (V == V_EXACT_SCALAR) {
-        geo = reinterpret_cast<const float4 *>(p.sph_geo);
+        blob = p.blob;
     } else {
-        const float4 *src = reinterpret_cast<const float4 *>(p.sph_geo);
-        for (uint32_t i = threadIdx.x; i < p.n_spheres_padded; i += blockDim.x) lds_geo[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < p.blob_units; i += blockDim.x) lds_blob[i] = p.blob[i];
         __syncthreads();
-        geo = lds_geo;
+        blob = lds_blob;
     }
+    const float4 *geo = blob;
+    const uint32_t *sidx = reinterpret_cast<const uint32_t *>(blob + p.n_geo);
+    const float4 *clus = blob + p.clus_offset;
 
     const uint32_t lane = threadIdx.x & 63u;
     const float fW = (float)p.W, fH = (float)p.H;
@@ -218,7 +261,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     f3 o = mk(0.f, 0.f, 0.f), d = o, att = o, pair = o, c2 = o;
     uint32_t depth = 0;
     uint64_t rng = 0;
-    unsigned long long segs = 0;
+    unsigned long long segs = 0, tests_sph = 0, tests_box = 0;
     Dbg dbg{0, 0, 0, 0};
     uint32_t dbg_iters = 0, dbg_refills = 0;
 
@@ -295,10 +338,14 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 done = true;  // main.cxx:74 (only reachable with max_depth == 0)
             } else {
                 ++segs;
-                float t;
-                const int ib = closest_hit<V, BLOCK, STATS>(p, geo, o, d, t, dbg);
+                uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
+                const Hit h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally);
+                tests_sph += p.n_always + (tally >> 16);
+                tests_box += (tally & 0xffffu) - p.n_always;
+                const float t = h.t;
+                const uint32_t ib = h.id;
                 ++depth;
-                if (ib < 0) {
+                if (ib == 0xffffffffu) {
                     // main.cxx:71: background(.5 * unit_direction.y + 1) * attenuation
                     const float tt = .5f * normalize(d).y + 1.f;
                     const f3 bg = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
@@ -378,10 +425,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     }
 
     if (p.segments) {
-        // wave reduction, one atomic per wave
-        unsigned long long v = segs;
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) atomicAdd(p.segments, v);
+        // wave reductions, one atomic per wave and counter: [0] segments, [1] sphere tests,
+        // [2] cluster box tests (lane-level, executed)
+        const unsigned long long c[3] = {segs, tests_sph, tests_box};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            unsigned long long v = c[i];
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) atomicAdd(p.segments + i, v);
+        }
     }
     if (STATS && p.dbg) {
         const uint32_t c[7] = {dbg_iters, dbg_refills, dbg.wave_blocks, dbg.lane_blocks, dbg.wave_roots,
@@ -450,41 +502,37 @@ __global__ __launch_bounds__(256) void epilogue_rgb8_kernel(const float *in, uin
 }
 
 // ---- launchers (called from rt_host.cpp) ---------------------------------------------
-// variant = scene source (V_EXACT_LDS / V_EXACT_SCALAR) x sphere block (2, 4, 8).
-template <int V, int B> static const void *kernel_ptr() { return reinterpret_cast<const void *>(&render_kernel<V, B, false>); }
-
-static const void *render_ptr(int variant, int block)
+static const void *render_ptr(int variant, bool cull)
 {
-    if (variant == V_STATS_LDS) return reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, 8, true>);
-    if (variant == V_FAST_LDS) {
-        if (block == 2) return kernel_ptr<V_FAST_LDS, 2>();
-        if (block == 4) return kernel_ptr<V_FAST_LDS, 4>();
-        if (block == 8) return kernel_ptr<V_FAST_LDS, 8>();
+    switch (variant) {
+    case V_EXACT_LDS:
+        return cull ? reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, true, false>)
+                    : reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, false, false>);
+    case V_FAST_LDS:
+        return cull ? reinterpret_cast<const void *>(&render_kernel<V_FAST_LDS, true, false>)
+                    : reinterpret_cast<const void *>(&render_kernel<V_FAST_LDS, false, false>);
+    case V_EXACT_SCALAR:
+        return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, false, false>);
+    case V_STATS_LDS:
+        return cull ? reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, true, true>)
+                    : reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, false, true>);
+    default:
+        return nullptr;
     }
-    if (variant == V_EXACT_LDS) {
-        if (block == 2) return kernel_ptr<V_EXACT_LDS, 2>();
-        if (block == 4) return kernel_ptr<V_EXACT_LDS, 4>();
-        if (block == 8) return kernel_ptr<V_EXACT_LDS, 8>();
-    } else if (variant == V_EXACT_SCALAR) {
-        if (block == 2) return kernel_ptr<V_EXACT_SCALAR, 2>();
-        if (block == 4) return kernel_ptr<V_EXACT_SCALAR, 4>();
-        if (block == 8) return kernel_ptr<V_EXACT_SCALAR, 8>();
-    }
-    return nullptr;
 }
 
-hipError_t launch_render(int variant, int block, const KParams &p, uint32_t grid, hipStream_t stream)
+hipError_t launch_render(int variant, bool cull, const KParams &p, uint32_t grid, hipStream_t stream)
 {
-    const void *fn = render_ptr(variant, block);
+    const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;
-    const size_t lds = (variant == V_EXACT_SCALAR) ? 0 : (size_t)p.n_spheres_padded * 16u;
+    const size_t lds = (variant == V_EXACT_SCALAR) ? 0 : (size_t)p.blob_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};
     return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, stream);
 }
 
-hipError_t occupancy_render(int variant, int block, int *blocks_per_cu, size_t lds)
+hipError_t occupancy_render(int variant, bool cull, int *blocks_per_cu, size_t lds)
 {
-    const void *fn = render_ptr(variant, block);
+    const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
 }

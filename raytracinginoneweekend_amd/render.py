@@ -15,9 +15,9 @@ from .camera import Camera
 
 
 def make_params(width, height, spp, max_depth=64, seed=1234, row_offset=0, row_stride=1, num_rows=0,
-                full_frame=False, scalar_scene=False, fast_math=False):
+                full_frame=False, scalar_scene=False, fast_math=False, brute_force=False):
     flags = (abi.RT_FLAG_FULL_FRAME if full_frame else 0) | (abi.RT_FLAG_SCALAR_SCENE if scalar_scene else 0) \
-        | (abi.RT_FLAG_FAST_MATH if fast_math else 0)
+        | (abi.RT_FLAG_FAST_MATH if fast_math else 0) | (abi.RT_FLAG_BRUTE_FORCE if brute_force else 0)
     return abi.RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, num_rows, flags)
 
 
@@ -85,7 +85,8 @@ class DeviceScene:
         self.device = device
 
     def render(self, camera, params, d_rgb, stream=None, d_segments=None):
-        """Enqueue a render into device pointer d_rgb (int address) on `stream` (int handle)."""
+        """Enqueue a render into device pointer d_rgb (int address) on `stream` (int handle).
+        d_segments: optional device int64[3] accumulating {segments, sphere tests, box tests}."""
         check(lib().rt_render_device(self.handle, C.byref(_cam(camera, params)), C.byref(params),
                                      C.c_void_p(d_rgb), C.c_void_p(stream or 0),
                                      C.c_void_p(d_segments) if d_segments else None))

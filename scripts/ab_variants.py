@@ -21,35 +21,34 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="lds:2,lds:4,lds:8,scalar:2,scalar:4,scalar:8")
+ap.add_argument("--variants", default="exact:cull,exact:brute,fast:cull,fast:brute")
 a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H, rt.CORRECTED if a.camera == "corrected" else rt.REFERENCE)
 ds = rt.DeviceScene(arrays)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-seg = torch.zeros(1, dtype=torch.int64, device="cuda")
+seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
 variants = [v.split(":") for v in a.variants.split(",")]
 times = {f"{k}:{b}": [] for k, b in variants}
 ref = None
 segs = {}
 for r in range(a.rounds + 1):
-    for kind, block in variants:
-        os.environ["RT_SPHERE_BLOCK"] = block
-        extra = {"fast_math": True} if kind.startswith("fast") else {}
-        p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind.endswith("scalar"), **extra)
+    for kind, trav in variants:
+        p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
+                           brute_force=trav == "brute")
         seg.zero_()
         ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr())
         torch.cuda.synchronize()
         ms = ds.kernel_times(1)[0]
-        name = f"{kind}:{block}"
+        name = f"{kind}:{trav}"
         if r == 0:  # warm-up round: check bits
             img = out.cpu()
             if ref is None:
                 ref = img
             same = torch.equal(img.view(torch.int32), ref.view(torch.int32))
-            segs[name] = int(seg.item())
+            segs[name] = [int(x) for x in seg.tolist()]
             d = (img - ref).abs()
             px = d.amax(dim=-1)
             print(f"{name}: identical={same} segments={segs[name]} max|d|={d.max().item():.3g} "
@@ -64,5 +63,7 @@ for name, t in times.items():
     prim = W * H * spp
     res[name] = {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
                  "mrays": round(prim / statistics.median(t) / 1e3, 1),
-                 "tflops": round(segs[name] * len(arrays[0]) * 20 / statistics.median(t) / 1e9, 2)}
+                 "exec_tflops": round((segs[name][1] * 20 + segs[name][2] * 19) / statistics.median(t) / 1e9, 2),
+                 "tests_per_seg": round(segs[name][1] / segs[name][0], 1),
+                 "boxes_per_seg": round(segs[name][2] / segs[name][0], 1)}
     print(name, json.dumps(res[name]), flush=True)

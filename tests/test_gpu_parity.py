@@ -17,7 +17,7 @@ from raytracinginoneweekend_amd import _abi as abi
 pytestmark = pytest.mark.gpu
 
 RENDERS = sorted(n for n, m in G.manifest()["renders"].items() if m["rng"] == "pcg")
-VARIANTS = {"lds": {}, "scalar": {"scalar_scene": True}}
+VARIANTS = {"clustered": {}, "brute": {"brute_force": True}, "scalar": {"scalar_scene": True}}
 
 
 def _params(meta, **kw):
@@ -142,7 +142,7 @@ def test_device_api_matches_host_api():
     host, _ = rt.render_f32((s, m), p)
     ds = rt.DeviceScene((s, m), device=0)
     out = torch.empty((72, 128, 3), dtype=torch.float32, device="cuda:0")
-    seg = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    seg = torch.zeros(3, dtype=torch.int64, device="cuda:0")
     stream = torch.cuda.current_stream()
     cam = rt.Camera.default(128, 72)
     for _ in range(2):  # workspace reuse across calls
@@ -150,13 +150,55 @@ def test_device_api_matches_host_api():
         ds.render(cam, p, out.data_ptr(), stream.cuda_stream, seg.data_ptr())
     torch.cuda.synchronize()
     _bits_equal(out.cpu().numpy(), host)
-    assert int(seg.item()) > 128 * 72 * 4
+    assert int(seg[0].item()) > 128 * 72 * 4
     u8 = torch.empty((72, 128, 3), dtype=torch.uint8, device="cuda:0")
     rt.epilogue_rgb8_device(out.data_ptr(), u8.data_ptr(), 128 * 72, stream.cuda_stream)
     torch.cuda.synchronize()
     ref8 = O.epilogue_rgb8(host)
     assert np.abs(u8.cpu().numpy().astype(int) - ref8.astype(int)).max() <= 1
     ds.close()
+
+
+def _random_scene(rng, n, spread, center=(0.0, 0.0, 0.0)):
+    """Adversarial scene: small spheres of mixed radii (some negative), exact duplicates with
+    different materials (equal hit times in different clusters), a few big spheres."""
+    s = np.zeros(n, dtype=abi.SPHERE_DTYPE)
+    m = np.zeros(7, dtype=abi.MATERIAL_DTYPE)
+    for i in range(7):
+        m[i] = (i % 3, rng.uniform(0.2, 1.0, 3).astype(np.float32), [0.0, 0.3, 1.5][i % 3])
+    c = (rng.uniform(-spread, spread, (n, 3)) + np.array(center)).astype(np.float32)
+    c[:, 1] = np.abs(c[:, 1]) * 0.2 + center[1]
+    r = rng.choice([0.05, 0.2, 0.3, 0.01], n).astype(np.float32)
+    r[rng.random(n) < 0.05] *= -1
+    s["center"], s["radius"], s["material"] = c, r, rng.integers(0, 7, n)
+    dup = rng.choice(n, n // 10, replace=False)
+    s["center"][dup[1::2]] = s["center"][dup[0::2][:len(dup[1::2])]]
+    s["radius"][dup[1::2]] = s["radius"][dup[0::2][:len(dup[1::2])]]
+    s["center"][0], s["radius"][0], s["material"][0] = (0, -1000.125, 0), 1000.0, 3
+    s["center"][1], s["radius"][1], s["material"][1] = (center[0], 1 + center[1], center[2]), 1.0, 2
+    return s, m
+
+
+@pytest.mark.parametrize("seed,n,spread,center,mode", [
+    (1, 600, 8.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
+    (2, 1500, 30.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_REFERENCE),
+    (3, 400, 3.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
+    (4, 800, 5.0, (200.0, 0.0, -150.0), abi.RT_CAMERA_CORRECTED),
+])
+def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode):
+    rng = np.random.default_rng(seed)
+    s, m = _random_scene(rng, n, spread, center)
+    W, H, spp = 48, 32, 4
+    cam = O.camera_default(W, H, mode)
+    p = rt.make_params(W, H, spp, 64, seed)
+    culled, st = rt.render_f32((s, m), p, cam)
+    brute, sb = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, seed, brute_force=True), cam)
+    _bits_equal(culled, brute)
+    assert st.segments == sb.segments
+    assert st.sphere_tests < sb.sphere_tests and st.box_tests > 0
+    ref, seg = O.render_f32(s, m, cam, p)
+    _bits_equal(culled, ref)
+    assert st.segments == seg
 
 
 # ---- fast-math kernel: stated tolerance (SURVEY.md §8c "performance build") ---------------

@@ -16,7 +16,18 @@ namespace rt {
 //   items of one launch: slots [slot_begin, slot_end) x all pixels, item I -> slot
 //     slot_begin + I / n_pixels, pixel I % n_pixels. Chunks of 64 consecutive items are
 //     dealt from 8 queues (chunk c belongs to queue c % 8) by per-queue atomic counters.
+// Per-render constants used only where a sample or an item starts (the kernel re-reads them
+// from the kernarg segment at each use; see render_kernel).
+struct FrameConsts {
+    float org[3], llc[3], hor[3], ver[3];
+    float lens, fW, fH;
+    uint32_t corrected, W, spp;
+    uint32_t inc_data_lo, inc_data_hi, inc_cam_lo, inc_cam_hi;
+    uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, g4, slot_begin, pad_;
+};
+
 struct KParams {
+    FrameConsts fc;
     // camera basis (rt_camera)
     float org[3], llc[3], hor[3], ver[3];
     float lens;
@@ -40,10 +51,10 @@ struct KParams {
     const float4 *blob;
     uint32_t blob_units;     // 16-byte units
     uint32_t n_geo, n_always, n_clusters, clus_offset;
-    const float *sph_full;   // [n_spheres][4] = cx, cy, cz, r
-    const uint32_t *sph_mat; // [n_spheres]
-    const float *mat_data;   // [n_materials][4] = albedo rgb, param
-    const uint32_t *mat_kind;
+    float clus_pad;          // max over clusters of 1e-3 * (|C|_1 + |e|_1) + 1e-6 (per-ray pad adds 1e-3 |o|_1)
+    // per-sphere hit record joined with its material, indexed by original sphere index:
+    // {cx, cy, cz, r}, {albedo rgb, param}, {kind, 0, 0, 0}
+    const float4 *hitrec;
     // outputs / workspace
     float *slots;            // [slot_end - slot_begin][n_pixels][3]
     uint32_t *queue_ctr;     // [8]

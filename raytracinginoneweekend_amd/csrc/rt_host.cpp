@@ -21,8 +21,8 @@
 #include "rt_device.h"
 
 namespace rt {
-hipError_t launch_render(int variant, bool cull, const KParams &p, uint32_t grid, hipStream_t stream);
-hipError_t occupancy_render(int variant, bool cull, int *blocks_per_cu, size_t lds);
+hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream);
+hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_t stream);
 } // namespace rt
@@ -64,13 +64,13 @@ constexpr uint32_t kMaxSlotsBytes = 1u << 31;  // slot workspace per pass (2 GiB
 struct rt_scene {
     int device = 0;
     uint32_t n_spheres = 0, n_materials = 0;
-    float *full = nullptr, *mat_data = nullptr;
+    float *hitrec = nullptr;  // [n][3] float4: {c, r}, {albedo, param}, {kind}
     // scene blobs: [0] every sphere in index order (brute force), [1] big
     // spheres always tested + spatial clusters
     float *blob[2] = {nullptr, nullptr};
     uint32_t blob_units[2] = {0, 0}, n_geo[2] = {0, 0}, n_always[2] = {0, 0}, n_clusters[2] = {0, 0},
              clus_offset[2] = {0, 0};
-    uint32_t *sph_mat = nullptr, *mat_kind = nullptr;
+    float clus_pad[2] = {0.f, 0.f};
     // workspace
     float *slots = nullptr;
     size_t slots_bytes = 0;
@@ -78,7 +78,7 @@ struct rt_scene {
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;
     int cu_count = 0;
-    int occ[4][2];  // [variant][cull] blocks per CU, -1 = not queried
+    int occ[4][3];  // [variant][cull structure] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     size_t max_lds = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
@@ -215,6 +215,7 @@ struct scene_builder {
 struct blob_t {
     std::vector<float> data;  // 16-byte units
     uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0;
+    float clus_pad = 0.f;
 };
 
 constexpr float kPadRel = 1e-3f;      // must match RT_PAD_REL in rt_kernel.hip
@@ -299,6 +300,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
             E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
         }
         const float kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
+        b.clus_pad = std::max(b.clus_pad, kc);
         const uint32_t start = push(c);
         const uint32_t cnt = pad8(static_cast<uint32_t>(c.size()));
         uint32_t packed = start | (cnt << 16);
@@ -341,6 +343,40 @@ int check_params(const rt_params *p)
     if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE | RT_FLAG_BRUTE_FORCE))
         return fail(RT_ERR_INVALID, "params: unknown flag");
     return RT_OK;
+}
+
+void fill_frame_consts(rt::KParams &k)
+{
+    rt::FrameConsts &f = k.fc;
+    for (int c = 0; c < 3; ++c) { f.org[c] = k.org[c]; f.llc[c] = k.llc[c]; f.hor[c] = k.hor[c]; f.ver[c] = k.ver[c]; }
+    f.lens = k.lens;
+    f.fW = static_cast<float>(k.W);
+    f.fH = static_cast<float>(k.H);
+    f.corrected = k.corrected;
+    f.W = k.W;
+    f.spp = k.spp;
+    f.inc_data_lo = static_cast<uint32_t>(k.inc_data);
+    f.inc_data_hi = static_cast<uint32_t>(k.inc_data >> 32);
+    f.inc_cam_lo = static_cast<uint32_t>(k.inc_cam);
+    f.inc_cam_hi = static_cast<uint32_t>(k.inc_cam >> 32);
+    f.row_offset = k.row_offset;
+    f.row_stride = k.row_stride;
+    f.tiled_rows = k.tiled_rows;
+    f.tiles_x = k.tiles_x;
+    f.n_pixels = k.n_pixels;
+    f.g4 = k.g4;
+    f.slot_begin = k.slot_begin;
+    f.pad_ = 0;
+}
+
+// Culling loop structure: 1 = box then its spheres, cluster by cluster (default, measured
+// faster); 2 = every box first into per-lane masks, then the wave walks the union of the
+// masks (RT_CULL_STRUCTURE=2 selects it for A/B; same bits).
+int cull_structure()
+{
+    const char *e = std::getenv("RT_CULL_STRUCTURE");
+    const int v = e ? std::atoi(e) : 1;
+    return (v == 1 || v == 2) ? v : 1;
 }
 
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
@@ -392,8 +428,7 @@ int rt_scene_destroy(rt_scene *sc)
     (void)hipSetDevice(sc->device);
     for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
     for (auto e : sc->ev_end) (void)hipEventDestroy(e);
-    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->full, (void *)sc->mat_data, (void *)sc->sph_mat,
-                    (void *)sc->mat_kind, (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
+    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->hitrec, (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
     delete sc;
@@ -418,21 +453,16 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "rt_scene_create: bad device index");
     RT_HIP(hipSetDevice(device));
 
-    std::vector<float> full(std::max(n_spheres, 1u) * 4, 0.f);
-    std::vector<uint32_t> smat(std::max(n_spheres, 1u), 0u), kind(n_materials);
-    std::vector<float> md(static_cast<size_t>(n_materials) * 4);
+    std::vector<float> hit(static_cast<size_t>(std::max(n_spheres, 1u)) * 12, 0.f);
     for (uint32_t i = 0; i < n_spheres; ++i) {
         const rt_sphere &sp = spheres[i];
-        full[4 * i] = sp.center[0]; full[4 * i + 1] = sp.center[1]; full[4 * i + 2] = sp.center[2];
-        full[4 * i + 3] = sp.radius;
-        smat[i] = sp.material;
+        const rt_material &mt = materials[sp.material];
+        float *h = hit.data() + 12 * static_cast<size_t>(i);
+        h[0] = sp.center[0]; h[1] = sp.center[1]; h[2] = sp.center[2]; h[3] = sp.radius;
+        h[4] = mt.albedo[0]; h[5] = mt.albedo[1]; h[6] = mt.albedo[2]; h[7] = mt.param;
+        std::memcpy(h + 8, &mt.kind, 4);
     }
     blob_t blobs[2] = {build_blob(spheres, n_spheres, false), build_blob(spheres, n_spheres, true)};
-    for (uint32_t i = 0; i < n_materials; ++i) {
-        kind[i] = materials[i].kind;
-        md[4 * i] = materials[i].albedo[0]; md[4 * i + 1] = materials[i].albedo[1]; md[4 * i + 2] = materials[i].albedo[2];
-        md[4 * i + 3] = materials[i].param;
-    }
     rt_scene *sc = new rt_scene();
     for (auto &r : sc->occ) for (auto &x : r) x = -1;
     sc->device = device;
@@ -451,11 +481,9 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         sc->n_always[b] = blobs[b].n_always;
         sc->n_clusters[b] = blobs[b].n_clusters;
         sc->clus_offset[b] = blobs[b].clus_offset;
+        sc->clus_pad[b] = blobs[b].clus_pad;
     }
-    if (rc == RT_OK) rc = up((void **)&sc->full, full.data(), full.size() * 4);
-    if (rc == RT_OK) rc = up((void **)&sc->sph_mat, smat.data(), smat.size() * 4);
-    if (rc == RT_OK) rc = up((void **)&sc->mat_data, md.data(), md.size() * 4);
-    if (rc == RT_OK) rc = up((void **)&sc->mat_kind, kind.data(), kind.size() * 4);
+    if (rc == RT_OK) rc = up((void **)&sc->hitrec, hit.data(), hit.size() * 4);
     if (rc == RT_OK) {
         hipError_t e = hipMalloc((void **)&sc->queue_ctr, 8 * sizeof(uint32_t));
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -526,10 +554,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.n_slots = k.g4 + P.spp % 4u;
     k.n_spheres = sc->n_spheres;
     k.n_materials = sc->n_materials;
-    k.sph_full = sc->full;
-    k.sph_mat = sc->sph_mat;
-    k.mat_data = sc->mat_data;
-    k.mat_kind = sc->mat_kind;
+    k.hitrec = reinterpret_cast<const float4 *>(sc->hitrec);
     k.queue_ctr = sc->queue_ctr;
     k.segments = reinterpret_cast<unsigned long long *>(d_segments);
 
@@ -551,16 +576,18 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         k.dbg = sc->dbg;
     }
     const int b = cull ? 1 : 0;
+    const int cull_mode = cull ? cull_structure() : 0;
     k.blob = reinterpret_cast<const float4 *>(sc->blob[b]);
     k.blob_units = sc->blob_units[b];
     k.n_geo = sc->n_geo[b];
     k.n_always = sc->n_always[b];
     k.n_clusters = sc->n_clusters[b];
     k.clus_offset = sc->clus_offset[b];
+    k.clus_pad = sc->clus_pad[b];
     const size_t lds = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(k.blob_units) * 16u;
-    int &occ = sc->occ[variant][b];
+    int &occ = sc->occ[variant][cull_mode];
     if (occ < 0) {
-        RT_HIP(rt::occupancy_render(variant, cull, &occ, lds));
+        RT_HIP(rt::occupancy_render(variant, cull_mode, &occ, lds));
         occ = std::max(occ, 1);
     }
 
@@ -585,7 +612,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_chunks + 3u) / 4u)));
         RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * sizeof(uint32_t), st));
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
-        RT_HIP(rt::launch_render(variant, cull, k, grid, st));
+        fill_frame_consts(k);
+        RT_HIP(rt::launch_render(variant, cull_mode, k, grid, st));
         if (s1 == k.n_slots) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
         rt::KAccum a{};
         a.slots = sc->slots;

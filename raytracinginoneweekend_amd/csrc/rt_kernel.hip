@@ -102,19 +102,20 @@ __device__ __forceinline__ float schlick(float ri, float c)
 }
 
 // ---- work decomposition ----------------------------------------------------------------
-__device__ __forceinline__ void pixel_of(const KParams &p, uint32_t i, uint32_t &x, uint32_t &rr)
+__device__ __forceinline__ void pixel_of(uint32_t W, uint32_t tiled_rows, uint32_t tiles_x, uint32_t i, uint32_t &x,
+                                         uint32_t &rr)
 {
-    const uint32_t tiled_px = p.tiled_rows * p.W;
+    const uint32_t tiled_px = tiled_rows * W;
     if (i < tiled_px) {
         uint32_t t = i >> 6, w = i & 63u;
-        uint32_t ty = t / p.tiles_x, tx = t - ty * p.tiles_x;
+        uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
         x = tx * 8u + (w & 7u);
         rr = ty * 8u + (w >> 3);
     } else {
         uint32_t j = i - tiled_px;
-        rr = j / p.W;
-        x = j - rr * p.W;
-        rr += p.tiled_rows;
+        rr = j / W;
+        x = j - rr * W;
+        rr += tiled_rows;
     }
 }
 
@@ -129,7 +130,7 @@ __device__ __forceinline__ void pixel_of(const KParams &p, uint32_t i, uint32_t 
 // Diagnostic counters (STATS builds only; see rt_scene_debug_counters): per-lane tallies
 // plus wave-level ones counted by the first active lane.
 struct Dbg {
-    uint32_t wave_blocks, lane_blocks, wave_roots, lane_roots;
+    uint32_t wave_blocks, lane_blocks, wave_roots, lane_roots, wave_member_blocks;
 };
 __device__ __forceinline__ bool first_active_lane()
 {
@@ -184,11 +185,15 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
 
 // Cluster culling: a lane tests a cluster's spheres only if its ray segment (kMIN, t_best]
 // can reach the cluster's AABB grown by a pad that dominates every float error involved
-// (1e-3 x (|o|_1 + |C|_1 + |e|_1) against errors below 3e-4 of that), so a
-// culled cluster never holds a sphere whose exact candidate could win: same bits.
+// (1e-3 x (|o|_1 + max_c(|C|_1 + |e|_1)) against errors below 3e-4 of that),
+// so a culled cluster never holds a sphere whose exact candidate could win: same bits.
+// All boxes of a group of 32 clusters are tested first (straight-line, LDS reads batched)
+// into a per-lane pass mask; the wave walks the union of the masks with a scalar loop and
+// each lane runs a cluster's spheres only if its own bit is set.
 #define RT_PAD_REL 1e-3f
+#define RT_MAX_CLUSTERS 128  // rt_host.cpp sizes clusters so a scene never needs more
 
-template <bool FAST, bool CULL, bool STATS>
+template <bool FAST, int CULL, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
                                            f3 d, Dbg &dbg, uint32_t &tests)
@@ -204,20 +209,70 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float ix = safe_rcp(d.x), iy = safe_rcp(d.y), iz = safe_rcp(d.z);
         const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
         const float aix = fabsf(ix), aiy = fabsf(iy), aiz = fabsf(iz);
-        const float opad = RT_PAD_REL * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z));
-        for (uint32_t c = 0; c < p.n_clusters; ++c) {
-            const float4 c0 = clus[2 * c], c1 = clus[2 * c + 1];   // {C, ex}, {ey, ez, kc, start|count}
-            const float pad = opad + c1.z;
-            const float hx = (c0.w + pad) * aix, hy = (c1.x + pad) * aiy, hz = (c1.y + pad) * aiz;
-            const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
-            const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
-            const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
-            ++tests;  // box tests are tallied in the high half (see below)
-            if (tin <= tout && tout >= 0.5f * RT_TMIN && tin <= h.t * 1.002f) {
-                const uint32_t sc = __builtin_amdgcn_readfirstlane(__float_as_uint(c1.w));
-                const uint32_t start = sc & 0xffffu, cnt = sc >> 16;
-                for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
-                tests += cnt << 16;
+        const float pad = fmaf(RT_PAD_REL, fabsf(o.x) + fabsf(o.y) + fabsf(o.z), p.clus_pad);
+        const float px = pad * aix, py = pad * aiy, pz = pad * aiz;
+        const float tb_hi = h.t * 1.002f;
+        const float t_lo = 0.5f * RT_TMIN;
+        if (CULL == 1) {  // interleaved: box, then its spheres, one cluster after another
+            for (uint32_t c = 0; c < p.n_clusters; ++c) {
+                const float4 c0 = clus[2 * c], c1 = clus[2 * c + 1];
+                const float hx = fmaf(c0.w, aix, px), hy = fmaf(c1.x, aiy, py), hz = fmaf(c1.y, aiz, pz);
+                const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
+                const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+                const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+                if (tin <= tout && tout >= t_lo && tin <= h.t * 1.002f) {
+                    const uint32_t sc = __builtin_amdgcn_readfirstlane(__float_as_uint(c1.w));
+                    const uint32_t start = sc & 0xffffu, cnt = sc >> 16;
+                    if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
+                    for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                    tests += cnt << 16;
+                }
+            }
+            tests += p.n_clusters;
+            return h;
+        }
+        // pass 1: every box (<= RT_MAX_CLUSTERS), masks per group of 32
+        uint32_t masks[RT_MAX_CLUSTERS / 32], unions[RT_MAX_CLUSTERS / 32];
+#pragma unroll
+        for (uint32_t gi = 0; gi < RT_MAX_CLUSTERS / 32; ++gi) {
+            const uint32_t g = gi * 32;
+            uint32_t mask = 0, any = 0;  // any: wave union, from ballots (active lanes only)
+            if (g < p.n_clusters) {
+                const uint32_t ng = min(32u, p.n_clusters - g);
+
+#pragma unroll 1
+                for (uint32_t c = 0; c < ng; ++c) {
+                    const float4 c0 = clus[2 * (g + c)], c1 = clus[2 * (g + c) + 1];  // {C, ex}, {ey, ez, -, start|count}
+                    const float hx = fmaf(c0.w, aix, px), hy = fmaf(c1.x, aiy, py), hz = fmaf(c1.y, aiz, pz);
+                    const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
+                    const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+                    const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+                    const bool pass = tin <= tout && tout >= t_lo && tin <= tb_hi;
+                    mask |= pass ? (1u << c) : 0u;
+                    any |= __ballot(pass) ? (1u << c) : 0u;
+                }
+            }
+            masks[gi] = mask;
+            unions[gi] = any;
+        }
+        tests += p.n_clusters;
+        // pass 2: the wave walks the union of the lanes' masks
+#pragma unroll
+        for (uint32_t gi = 0; gi < RT_MAX_CLUSTERS / 32; ++gi) {
+            const uint32_t g = gi * 32;
+            if (g >= p.n_clusters) break;
+            const uint32_t mask = masks[gi];
+            uint32_t u = __builtin_amdgcn_readfirstlane(unions[gi]);
+            while (u) {
+                const uint32_t c = __builtin_ctz(u);
+                u &= u - 1u;
+                if (mask & (1u << c)) {
+                    const uint32_t sc = __float_as_uint(clus[2 * (g + c) + 1].w);
+                    const uint32_t start = __builtin_amdgcn_readfirstlane(sc & 0xffffu);
+                    const uint32_t cnt = __builtin_amdgcn_readfirstlane(sc >> 16);
+                    for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                    tests += cnt << 16;
+                }
             }
         }
     }
@@ -228,7 +283,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
 #endif
-template <int V, bool CULL, bool STATS>
+template <int V, int CULL, bool STATS>
 __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(const KParams p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
@@ -243,12 +298,19 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         __syncthreads();
         blob = lds_blob;
     }
+    // Per-render constants used only where a sample or an item starts are re-read from the
+    // kernarg segment at each use (scalar loads) through a pointer made opaque every loop
+    // iteration, so they do not pin ~30 SGPRs for the whole kernel (SGPR count bounds the
+    // workgroups per CU on gfx950).
+    typedef const __attribute__((address_space(4))) FrameConsts *fc_ptr_t;
+    const fc_ptr_t fc_base =
+        (fc_ptr_t)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() +
+                   offsetof(KParams, fc));
     const float4 *geo = blob;
     const uint32_t *sidx = reinterpret_cast<const uint32_t *>(blob + p.n_geo);
     const float4 *clus = blob + p.clus_offset;
 
     const uint32_t lane = threadIdx.x & 63u;
-    const float fW = (float)p.W, fH = (float)p.H;
 
     // wave-uniform cursor over the item space
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
@@ -257,15 +319,18 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
 
     // lane state
     bool has_item = false, alive = false;
-    uint32_t px = 0, py = 0, pix = 0, slot = 0, s_first = 0, s_count = 0, j = 0;
+    // item: pixel enumeration index + slot (low 24 bits) | sample-within-item j (bits 24-26)
+    uint32_t pix = 0, slotj = 0;
     f3 o = mk(0.f, 0.f, 0.f), d = o, att = o, pair = o, c2 = o;
     uint32_t depth = 0;
     uint64_t rng = 0;
-    unsigned long long segs = 0, tests_sph = 0, tests_box = 0;
-    Dbg dbg{0, 0, 0, 0};
+    uint32_t segs = 0, tests_sph = 0, tests_box = 0;  // per-lane tallies (widened at the end)
+    Dbg dbg{0, 0, 0, 0, 0};
     uint32_t dbg_iters = 0, dbg_refills = 0;
 
     for (;;) {
+        fc_ptr_t fc = fc_base;
+        asm volatile("" : "+s"(fc));
         // ---- refill items for idle lanes -------------------------------------------
         uint64_t need = __ballot(!has_item);
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
@@ -288,15 +353,10 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (!has_item && rank < avail) {
                 const uint32_t I = cnext + rank;
-                const uint32_t ls = I / p.n_pixels;
-                pix = I - ls * p.n_pixels;
-                slot = p.slot_begin + ls;
-                uint32_t rr;
-                pixel_of(p, pix, px, rr);
-                py = p.row_offset + rr * p.row_stride;
-                if (slot < p.g4) { s_first = slot * 4u; s_count = 4u; }
-                else { s_first = p.g4 * 4u + (slot - p.g4); s_count = 1u; }
-                j = 0;
+                const uint32_t n_pixels = fc->n_pixels;
+                const uint32_t ls = I / n_pixels;
+                pix = I - ls * n_pixels;
+                slotj = fc->slot_begin + ls;
                 has_item = true;
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
@@ -306,23 +366,30 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
 
         // ---- start a sample on lanes that have an item but no live path -------------
         if (has_item && !alive) {
-            const uint32_t s = s_first + j;
-            const uint64_t key = ((uint64_t)py * p.W + px) * p.spp + s;
-            rng = pcg_seed(key, p.inc_data);
-            uint64_t rc = pcg_seed(key, p.inc_cam);
+            uint32_t px, rr;
+            pixel_of(fc->W, fc->tiled_rows, fc->tiles_x, pix, px, rr);
+            const uint32_t py = fc->row_offset + rr * fc->row_stride;
+            const uint32_t slot = slotj & 0xffffffu, j = slotj >> 24, g4 = fc->g4;
+            const uint32_t s = slot < g4 ? slot * 4u + j : g4 * 4u + (slot - g4);
+            const uint64_t key = ((uint64_t)py * fc->W + px) * fc->spp + s;
+            const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
+            const uint64_t inc_cam = ((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo;
+            rng = pcg_seed(key, inc_data);
+            uint64_t rc = pcg_seed(key, inc_cam);
             // main.cxx:192-200
+            const float fW = fc->fW, fH = fc->fH;
             const float u = (float)px / fW;
             const float v = (float)py / fH;
-            const float uu = u + canonical(rng, p.inc_data) / fW;
-            const float vv = v + canonical(rng, p.inc_data) / fH;
+            const float uu = u + canonical(rng, inc_data) / fW;
+            const float vv = v + canonical(rng, inc_data) / fH;
             // camera.hxx:46-57
-            const f3 rd = random_in_unit_sphere(rc, p.inc_cam) * p.lens;
+            const f3 rd = random_in_unit_sphere(rc, inc_cam) * fc->lens;
             const f3 off = mk(uu * rd.x, vv * rd.y, 0.f);
-            const f3 org = mk(p.org[0], p.org[1], p.org[2]);
+            const f3 org = mk(fc->org[0], fc->org[1], fc->org[2]);
             o = org + off;
-            d = ((mk(p.llc[0], p.llc[1], p.llc[2]) + mk(p.hor[0], p.hor[1], p.hor[2]) * uu) +
-                 mk(p.ver[0], p.ver[1], p.ver[2]) * (1.f - vv)) - off;
-            if (p.corrected) d = d - org;
+            d = ((mk(fc->llc[0], fc->llc[1], fc->llc[2]) + mk(fc->hor[0], fc->hor[1], fc->hor[2]) * uu) +
+                 mk(fc->ver[0], fc->ver[1], fc->ver[2]) * (1.f - vv)) - off;
+            if (fc->corrected) d = d - org;
             att = mk(1.f, 1.f, 1.f);
             depth = 0;
             alive = true;
@@ -352,22 +419,22 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     col = bg * att;
                     done = true;
                 } else {
-                    const float4 sf = reinterpret_cast<const float4 *>(p.sph_full)[ib];
+                    const float4 sf = p.hitrec[3 * ib];
                     const f3 ctr = mk(sf.x, sf.y, sf.z);
                     const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
                     const f3 hn = (hp - ctr) / sf.w;            // raytracer.hxx:71
-                    const uint32_t mi = p.sph_mat[ib];
-                    const float4 md = reinterpret_cast<const float4 *>(p.mat_data)[mi];
-                    const uint32_t kind = p.mat_kind[mi];
+                    const float4 md = p.hitrec[3 * ib + 1];     // material of the sphere
+                    const uint32_t kind = __float_as_uint(p.hitrec[3 * ib + 2].x);
+                    const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
                     const f3 albedo = mk(md.x, md.y, md.z);
                     bool scattered = true;
                     f3 nd;
                     if (kind == 0u) {                           // lambert, raytracer.hxx:132-141
-                        const f3 r = random_in_unit_sphere(rng, p.inc_data);
+                        const f3 r = random_in_unit_sphere(rng, inc_data);
                         nd = ((hp + hn) + r) - hp;
                     } else if (kind == 1u) {                    // metal, raytracer.hxx:143-156
                         const f3 refl = reflect(normalize(d), hn);
-                        const f3 r = random_in_unit_sphere(rng, p.inc_data);
+                        const f3 r = random_in_unit_sphere(rng, inc_data);
                         nd = refl + r * md.w;
                         scattered = dot(nd, hn) > 0.f;
                     } else {                                    // dielectric, raytracer.hxx:158-194
@@ -383,7 +450,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                         const f3 refr = refract(ud, outward, ri);
                         float prob = 1.f;
                         if (length(refr) > 0.f) prob = schlick(ri, cosv);
-                        nd = canonical(rng, p.inc_data) < prob ? reflect(ud, hn) : refr;
+                        nd = canonical(rng, inc_data) < prob ? reflect(ud, hn) : refr;
                     }
                     if (!scattered) {
                         done = true;                            // main.cxx:68
@@ -400,7 +467,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 alive = false;
                 bool item_done = false;
                 f3 outv = col;
-                if (s_count == 1u) {
+                const uint32_t slot = slotj & 0xffffffu, j = slotj >> 24;
+                if (slot >= fc->g4) {
                     item_done = true;
                 } else if (j == 0u) {
                     pair = col;
@@ -412,9 +480,9 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     outv = pair + (c2 + col);
                     item_done = true;
                 }
-                ++j;
+                slotj += 1u << 24;
                 if (item_done) {
-                    float *dst = p.slots + ((size_t)(slot - p.slot_begin) * p.n_pixels + pix) * 3u;
+                    float *dst = p.slots + ((size_t)(slot - fc->slot_begin) * fc->n_pixels + pix) * 3u;
                     dst[0] = outv.x;
                     dst[1] = outv.y;
                     dst[2] = outv.z;
@@ -427,7 +495,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     if (p.segments) {
         // wave reductions, one atomic per wave and counter: [0] segments, [1] sphere tests,
         // [2] cluster box tests (lane-level, executed)
-        const unsigned long long c[3] = {segs, tests_sph, tests_box};
+        const unsigned long long c[3] = {segs, tests_sph, tests_box};  // widened before the reduction
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             unsigned long long v = c[i];
@@ -436,10 +504,10 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         }
     }
     if (STATS && p.dbg) {
-        const uint32_t c[7] = {dbg_iters, dbg_refills, dbg.wave_blocks, dbg.lane_blocks, dbg.wave_roots,
-                               dbg.lane_roots, (uint32_t)segs};
+        const uint32_t c[8] = {dbg_iters, dbg_refills, dbg.wave_blocks, dbg.lane_blocks, dbg.wave_roots,
+                               dbg.lane_roots, (uint32_t)segs, dbg.wave_member_blocks};
 #pragma unroll
-        for (int i = 0; i < 7; ++i) {
+        for (int i = 0; i < 8; ++i) {
             unsigned long long v = c[i];
             for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
             if (lane == 0) atomicAdd(p.dbg + i, v);
@@ -502,26 +570,25 @@ __global__ __launch_bounds__(256) void epilogue_rgb8_kernel(const float *in, uin
 }
 
 // ---- launchers (called from rt_host.cpp) ---------------------------------------------
-static const void *render_ptr(int variant, bool cull)
+template <int V, bool STATS> static const void *ptr3(int cull)
+{
+    if (cull == 1) return reinterpret_cast<const void *>(&render_kernel<V, 1, STATS>);
+    if (cull == 2) return reinterpret_cast<const void *>(&render_kernel<V, 2, STATS>);
+    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS>);
+}
+
+static const void *render_ptr(int variant, int cull)
 {
     switch (variant) {
-    case V_EXACT_LDS:
-        return cull ? reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, true, false>)
-                    : reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, false, false>);
-    case V_FAST_LDS:
-        return cull ? reinterpret_cast<const void *>(&render_kernel<V_FAST_LDS, true, false>)
-                    : reinterpret_cast<const void *>(&render_kernel<V_FAST_LDS, false, false>);
-    case V_EXACT_SCALAR:
-        return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, false, false>);
-    case V_STATS_LDS:
-        return cull ? reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, true, true>)
-                    : reinterpret_cast<const void *>(&render_kernel<V_EXACT_LDS, false, true>);
-    default:
-        return nullptr;
+    case V_EXACT_LDS: return ptr3<V_EXACT_LDS, false>(cull);
+    case V_FAST_LDS: return ptr3<V_FAST_LDS, false>(cull);
+    case V_EXACT_SCALAR: return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false>);
+    case V_STATS_LDS: return ptr3<V_EXACT_LDS, true>(cull);
+    default: return nullptr;
     }
 }
 
-hipError_t launch_render(int variant, bool cull, const KParams &p, uint32_t grid, hipStream_t stream)
+hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream)
 {
     const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;
@@ -530,7 +597,7 @@ hipError_t launch_render(int variant, bool cull, const KParams &p, uint32_t grid
     return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, stream);
 }
 
-hipError_t occupancy_render(int variant, bool cull, int *blocks_per_cu, size_t lds)
+hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds)
 {
     const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;

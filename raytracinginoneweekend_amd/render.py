@@ -102,8 +102,9 @@ class DeviceScene:
         """Counters of the instrumented kernel (RT_DEBUG_STATS=1), see rt_scene_debug_counters."""
         buf = (C.c_uint64 * 8)()
         check(lib().rt_scene_debug_counters(self.handle, buf, 1 if reset else 0))
-        keys = ["wave_iters", "wave_refills", "wave_blocks", "lane_blocks", "wave_roots", "lane_roots", "segments"]
-        return dict(zip(keys, list(buf)[:7]))
+        keys = ["wave_iters", "wave_refills", "wave_blocks", "lane_blocks", "wave_roots", "lane_roots", "segments",
+                "wave_member_blocks"]
+        return dict(zip(keys, list(buf)))
 
     def close(self):
         if self.handle:

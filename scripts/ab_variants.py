@@ -36,6 +36,8 @@ ref = None
 segs = {}
 for r in range(a.rounds + 1):
     for kind, trav in variants:
+        if trav.startswith("cull") and len(trav) > 4:
+            os.environ["RT_CULL_STRUCTURE"] = trav[4:]
         p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
                            brute_force=trav == "brute")
         seg.zero_()

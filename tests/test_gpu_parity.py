@@ -17,7 +17,8 @@ from raytracinginoneweekend_amd import _abi as abi
 pytestmark = pytest.mark.gpu
 
 RENDERS = sorted(n for n, m in G.manifest()["renders"].items() if m["rng"] == "pcg")
-VARIANTS = {"clustered": {}, "brute": {"brute_force": True}, "scalar": {"scalar_scene": True}}
+VARIANTS = {"clustered": {}, "clustered2": {"_structure": "2"}, "brute": {"brute_force": True},
+            "scalar": {"scalar_scene": True}}
 
 
 def _params(meta, **kw):
@@ -43,11 +44,14 @@ def _device():
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("name", RENDERS)
-def test_golden_render_f32(name, variant):
+def test_golden_render_f32(name, variant, monkeypatch):
     meta, f32, _ = G.render(name)
     scene = G.scene(meta["scene"])
     cam = rt.Camera.default(meta["width"], meta["height"], G.camera_mode(meta))
-    img, st = rt.render_f32(scene, _params(meta, **VARIANTS[variant]), cam)
+    kw = dict(VARIANTS[variant])
+    if "_structure" in kw:
+        monkeypatch.setenv("RT_CULL_STRUCTURE", kw.pop("_structure"))
+    img, st = rt.render_f32(scene, _params(meta, **kw), cam)
     _bits_equal(img, f32)
     assert st.primaries == meta["width"] * meta["num_rows"] * meta["spp"]
     assert st.segments >= st.primaries
@@ -185,7 +189,9 @@ def _random_scene(rng, n, spread, center=(0.0, 0.0, 0.0)):
     (3, 400, 3.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
     (4, 800, 5.0, (200.0, 0.0, -150.0), abi.RT_CAMERA_CORRECTED),
 ])
-def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode):
+@pytest.mark.parametrize("structure", ["1", "2"])
+def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, structure, monkeypatch):
+    monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
     rng = np.random.default_rng(seed)
     s, m = _random_scene(rng, n, spread, center)
     W, H, spp = 48, 32, 4

@@ -177,8 +177,9 @@ int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n)
  * instrumented kernel (identical output) that tallies: [0] wave loop iterations,
  * [1] wave refill rounds, [2] wave / [3] lane sphere blocks with a positive discriminant,
  * [4] wave / [5] lane root evaluations, [6] segments, [7] wave-level blocks of 8 cluster
- * members executed. Copies them out; reset != 0 zeroes.                               */
-int rt_scene_debug_counters(rt_scene *scene, uint64_t out[8], int reset);
+ * members executed, [8..12] shader-clock cycles summed over waves per loop region
+ * (refill, sample start, closest hit, shading, fold). Copies them out; reset zeroes.  */
+int rt_scene_debug_counters(rt_scene *scene, uint64_t out[16], int reset);
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,
                             void *stream);

@@ -570,8 +570,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     if (variant == rt::V_EXACT_LDS && debug_stats()) {
         variant = rt::V_STATS_LDS;
         if (!sc->dbg) {
-            RT_HIP(hipMalloc((void **)&sc->dbg, 8 * sizeof(unsigned long long)));
-            RT_HIP(hipMemset(sc->dbg, 0, 8 * sizeof(unsigned long long)));
+            RT_HIP(hipMalloc((void **)&sc->dbg, 16 * sizeof(unsigned long long)));
+            RT_HIP(hipMemset(sc->dbg, 0, 16 * sizeof(unsigned long long)));
         }
         k.dbg = sc->dbg;
     }
@@ -651,17 +651,17 @@ int rt_scene_kernel_times(rt_scene *sc, uint32_t max, float *ms, uint32_t *n)
     return RT_OK;
 }
 
-int rt_scene_debug_counters(rt_scene *sc, uint64_t out[8], int reset)
+int rt_scene_debug_counters(rt_scene *sc, uint64_t out[16], int reset)
 {
     if (!sc || !out) return fail(RT_ERR_INVALID, "rt_scene_debug_counters: null argument");
     RT_HIP(hipSetDevice(sc->device));
     if (!sc->dbg) {
-        std::memset(out, 0, 8 * sizeof(uint64_t));
+        std::memset(out, 0, 16 * sizeof(uint64_t));
         return RT_OK;
     }
     RT_HIP(hipDeviceSynchronize());
-    RT_HIP(hipMemcpy(out, sc->dbg, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    if (reset) RT_HIP(hipMemset(sc->dbg, 0, 8 * sizeof(uint64_t)));
+    RT_HIP(hipMemcpy(out, sc->dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (reset) RT_HIP(hipMemset(sc->dbg, 0, 16 * sizeof(uint64_t)));
     return RT_OK;
 }
 

@@ -327,8 +327,19 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     uint32_t segs = 0, tests_sph = 0, tests_box = 0;  // per-lane tallies (widened at the end)
     Dbg dbg{0, 0, 0, 0, 0};
     uint32_t dbg_iters = 0, dbg_refills = 0;
+    // STATS build only: shader-clock cycles per loop region, summed over the wave's iterations
+    uint64_t cyc[5] = {0, 0, 0, 0, 0};  // refill, sample start, closest hit, shading, fold
+    uint64_t t_prev = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int r) {
+        if (STATS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            cyc[r] += t - t_prev;
+            t_prev = t;
+        }
+    };
 
     for (;;) {
+        stamp(4);
         fc_ptr_t fc = fc_base;
         asm volatile("" : "+s"(fc));
         // ---- refill items for idle lanes -------------------------------------------
@@ -364,6 +375,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             need = __ballot(!has_item);
         }
 
+        stamp(0);
         // ---- start a sample on lanes that have an item but no live path -------------
         if (has_item && !alive) {
             uint32_t px, rr;
@@ -394,6 +406,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             depth = 0;
             alive = true;
         }
+        stamp(1);
         if (__ballot(alive) == 0) break;  // only when the item space is exhausted
         if (STATS && lane == 0) ++dbg_iters;
 
@@ -407,6 +420,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 ++segs;
                 uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
                 const Hit h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally);
+                stamp(2);
                 tests_sph += p.n_always + (tally >> 16);
                 tests_box += (tally & 0xffffu) - p.n_always;
                 const float t = h.t;
@@ -462,6 +476,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     }
                 }
             }
+            stamp(3);
             if (done) {
                 // fold the finished sample into its item (main.cxx:205 blocked reduce)
                 alive = false;
@@ -512,6 +527,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
             if (lane == 0) atomicAdd(p.dbg + i, v);
         }
+        if (lane == 0)
+            for (int i = 0; i < 5; ++i) atomicAdd(p.dbg + 8 + i, (unsigned long long)cyc[i]);
     }
 }
 

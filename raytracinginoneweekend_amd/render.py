@@ -100,10 +100,10 @@ class DeviceScene:
 
     def debug_counters(self, reset=True):
         """Counters of the instrumented kernel (RT_DEBUG_STATS=1), see rt_scene_debug_counters."""
-        buf = (C.c_uint64 * 8)()
+        buf = (C.c_uint64 * 16)()
         check(lib().rt_scene_debug_counters(self.handle, buf, 1 if reset else 0))
         keys = ["wave_iters", "wave_refills", "wave_blocks", "lane_blocks", "wave_roots", "lane_roots", "segments",
-                "wave_member_blocks"]
+                "wave_member_blocks", "cyc_refill", "cyc_start", "cyc_hit", "cyc_shade", "cyc_fold"]
         return dict(zip(keys, list(buf)))
 
     def close(self):

@@ -18,12 +18,19 @@ namespace rt {
 //     dealt from 8 queues (chunk c belongs to queue c % 8) by per-queue atomic counters.
 // Per-render constants used only where a sample or an item starts (the kernel re-reads them
 // from the kernarg segment at each use; see render_kernel).
+// Exact unsigned division by a per-render invariant d (Granlund-Montgomery, "round-up with
+// add"): q = (t + ((n - t) >> 1)) >> (l - 1), t = mulhi(n, m), for every 32-bit n.
+struct UDiv {
+    uint32_t m, l;   // l = ceil(log2 d) (>= 1), m = floor(2^32 (2^l - d) / d) + 1; d = 1: l = 0
+};
+
 struct FrameConsts {
     float org[3], llc[3], hor[3], ver[3];
     float lens, fW, fH;
     uint32_t corrected, W, spp;
     uint32_t inc_data_lo, inc_data_hi, inc_cam_lo, inc_cam_hi;
     uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, g4, slot_begin, pad_;
+    UDiv div_W, div_tiles_x, div_n_pixels;
 };
 
 struct KParams {

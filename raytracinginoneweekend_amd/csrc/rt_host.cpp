@@ -4,7 +4,9 @@
 //
 // Compiled with -ffp-contract=off: the camera basis and the huge-scene generator must round
 // exactly like the reference's (g++, x86-64 SSE, no contraction).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cfloat>
@@ -345,6 +347,17 @@ int check_params(const rt_params *p)
     return RT_OK;
 }
 
+rt::UDiv make_udiv(uint32_t d)
+{
+    rt::UDiv r{0, 0};
+    if (d <= 1) return r;  // d = 1: identity (l = 0)
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    r.l = l;
+    r.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    return r;
+}
+
 void fill_frame_consts(rt::KParams &k)
 {
     rt::FrameConsts &f = k.fc;
@@ -367,6 +380,9 @@ void fill_frame_consts(rt::KParams &k)
     f.g4 = k.g4;
     f.slot_begin = k.slot_begin;
     f.pad_ = 0;
+    f.div_W = make_udiv(k.W);
+    f.div_tiles_x = make_udiv(k.tiles_x);
+    f.div_n_pixels = make_udiv(k.n_pixels);
 }
 
 // Culling loop structure: 1 = box then its spheres, cluster by cluster (default, measured
@@ -752,10 +768,176 @@ int rt_render_rgb8(const rt_sphere *spheres, uint32_t n_spheres, const rt_materi
     return render_host(spheres, n_spheres, materials, n_materials, camera, params, nullptr, rgb_out, stats);
 }
 
-int rt_render_multi_f32(const rt_sphere *, uint32_t, const rt_material *, uint32_t, const rt_camera *,
-                        const rt_params *, int, float *, rt_stats *)
+} // extern "C"
+
+// ---- single-process multi-GPU render: interleaved row tiles + RCCL gather over xGMI -----
+// RCCL is opened with dlopen (librccl.so.1) on first use, so the library has no link-time
+// dependency on it and shares the process's RCCL if another component (torch) loaded it.
+namespace {
+struct rccl_api {
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    bool ok = false;
+};
+const rccl_api &rccl()
 {
-    return fail(RT_ERR_UNSUPPORTED, "rt_render_multi_f32: not built yet");
+    static rccl_api api = [] {
+        rccl_api a;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return a;
+        a.comm_init_all = reinterpret_cast<decltype(a.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+        a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        a.send = reinterpret_cast<decltype(a.send)>(dlsym(h, "ncclSend"));
+        a.recv = reinterpret_cast<decltype(a.recv)>(dlsym(h, "ncclRecv"));
+        a.group_start = reinterpret_cast<decltype(a.group_start)>(dlsym(h, "ncclGroupStart"));
+        a.group_end = reinterpret_cast<decltype(a.group_end)>(dlsym(h, "ncclGroupEnd"));
+        a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
+        a.ok = a.comm_init_all && a.comm_destroy && a.send && a.recv && a.group_start && a.group_end && a.error_string;
+        return a;
+    }();
+    return api;
+}
+} // namespace
+
+extern "C" {
+
+int rt_render_multi_f32(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
+                        uint32_t n_materials, const rt_camera *camera, const rt_params *params, int ngpu,
+                        float *rgb_out, rt_stats *stats)
+{
+    if (!camera || !rgb_out) return fail(RT_ERR_INVALID, "rt_render_multi_f32: null argument");
+    if (int rc = check_params(params); rc != RT_OK) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_DEVICE, "rt_render_multi_f32: no HIP device");
+    const int N = ngpu <= 0 ? ndev : std::min(ngpu, ndev);
+    const rt_params base = *params;
+    const uint32_t W = base.width, H = base.height;
+    // rank r renders rows y = r, r + N, ... (rows of the whole image; row_offset/num_rows ignored)
+    std::vector<uint32_t> rows(N);
+    for (int r = 0; r < N; ++r) rows[r] = static_cast<uint32_t>(r) < H ? (H - r + N - 1) / N : 0;
+    std::vector<rt_scene *> sc(N, nullptr);
+    std::vector<hipStream_t> st(N, nullptr);
+    std::vector<float *> tile(N, nullptr), recv(N, nullptr);
+    std::vector<uint64_t *> seg(N, nullptr);
+    std::vector<hipEvent_t> e0(N, nullptr), e1(N, nullptr);
+    std::vector<ncclComm_t> comms;
+    float *frame = nullptr;
+    int rc = RT_OK;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+        return rc == RT_OK;
+    };
+    for (int r = 0; r < N && rc == RT_OK; ++r) {
+        rc = rt_scene_create(spheres, n_spheres, materials, n_materials, r, &sc[r]);
+        if (rc != RT_OK) break;
+        chk(hipSetDevice(r), "hipSetDevice");
+        chk(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking), "hipStreamCreate");
+        chk(hipMalloc(&tile[r], std::max<size_t>(1, static_cast<size_t>(rows[r]) * W * 3) * 4), "hipMalloc");
+        chk(hipMalloc(&seg[r], 24), "hipMalloc");
+        chk(hipMemsetAsync(seg[r], 0, 24, st[r]), "hipMemsetAsync");
+        chk(hipEventCreate(&e0[r]), "hipEventCreate");
+        chk(hipEventCreate(&e1[r]), "hipEventCreate");
+        if (r == 0) chk(hipMalloc(&frame, static_cast<size_t>(H) * W * 3 * 4), "hipMalloc");
+        if (r > 0 && rc == RT_OK) {
+            chk(hipSetDevice(0), "hipSetDevice");
+            chk(hipMalloc(&recv[r], std::max<size_t>(1, static_cast<size_t>(rows[r]) * W * 3) * 4), "hipMalloc");
+        }
+    }
+    // render every tile concurrently
+    for (int r = 0; r < N && rc == RT_OK; ++r) {
+        if (!rows[r]) continue;
+        rt_params p = base;
+        p.row_offset = static_cast<uint32_t>(r);
+        p.row_stride = static_cast<uint32_t>(N);
+        p.num_rows = rows[r];
+        p.flags &= ~RT_FLAG_FULL_FRAME;
+        chk(hipSetDevice(r), "hipSetDevice");
+        chk(hipEventRecord(e0[r], st[r]), "hipEventRecord");
+        if (rc == RT_OK) rc = rt_render_device(sc[r], camera, &p, tile[r], st[r], seg[r]);
+        chk(hipEventRecord(e1[r], st[r]), "hipEventRecord");
+    }
+    // gather the tiles to device 0 over RCCL (one point-to-point transfer per peer link)
+    if (rc == RT_OK && N > 1) {
+        const rccl_api &api = rccl();
+        if (!api.ok) rc = fail(RT_ERR_COMM, "rt_render_multi_f32: librccl.so.1 not loadable");
+        std::vector<int> devs(N);
+        for (int r = 0; r < N; ++r) devs[r] = r;
+        comms.assign(N, nullptr);
+        if (rc == RT_OK) {
+            ncclResult_t nr = api.comm_init_all(comms.data(), N, devs.data());
+            if (nr != ncclSuccess) rc = fail(RT_ERR_COMM, std::string("ncclCommInitAll: ") + api.error_string(nr));
+        }
+        if (rc == RT_OK) {
+            ncclResult_t nr = api.group_start();
+            for (int r = 1; r < N && nr == ncclSuccess; ++r) {
+                if (!rows[r]) continue;
+                const size_t cnt = static_cast<size_t>(rows[r]) * W * 3;
+                nr = api.send(tile[r], cnt, ncclFloat, 0, comms[r], st[r]);
+                if (nr == ncclSuccess) nr = api.recv(recv[r], cnt, ncclFloat, r, comms[0], st[0]);
+            }
+            ncclResult_t ne = api.group_end();
+            if (nr == ncclSuccess) nr = ne;
+            if (nr != ncclSuccess) rc = fail(RT_ERR_COMM, std::string("RCCL gather: ") + api.error_string(nr));
+        }
+    }
+    // de-interleave on device 0: frame row r + i*N <- tile r row i (one strided copy per rank)
+    if (rc == RT_OK) {
+        chk(hipSetDevice(0), "hipSetDevice");
+        const size_t row_bytes = static_cast<size_t>(W) * 3 * 4;
+        for (int r = 0; r < N && rc == RT_OK; ++r) {
+            if (!rows[r]) continue;
+            chk(hipMemcpy2DAsync(frame + static_cast<size_t>(r) * W * 3, row_bytes * N, r == 0 ? tile[0] : recv[r],
+                                 row_bytes, row_bytes, rows[r], hipMemcpyDeviceToDevice, st[0]),
+                "hipMemcpy2DAsync");
+        }
+        chk(hipMemcpyAsync(rgb_out, frame, static_cast<size_t>(H) * W * 3 * 4, hipMemcpyDeviceToHost, st[0]),
+            "hipMemcpyAsync");
+    }
+    uint64_t segs[3] = {0, 0, 0};
+    double kms = 0.0;
+    for (int r = 0; r < N; ++r) {
+        if (rc == RT_OK && st[r]) {
+            chk(hipSetDevice(r), "hipSetDevice");
+            chk(hipStreamSynchronize(st[r]), "hipStreamSynchronize");
+            uint64_t v[3] = {0, 0, 0};
+            chk(hipMemcpy(v, seg[r], 24, hipMemcpyDeviceToHost), "hipMemcpy");
+            float ms = 0.f;
+            if (rows[r]) chk(hipEventElapsedTime(&ms, e0[r], e1[r]), "hipEventElapsedTime");
+            for (int i = 0; i < 3; ++i) segs[i] += v[i];
+            kms = std::max(kms, static_cast<double>(ms));
+        }
+    }
+    for (auto c : comms)
+        if (c) rccl().comm_destroy(c);
+    for (int r = 0; r < N; ++r) {
+        (void)hipSetDevice(r);
+        if (e0[r]) (void)hipEventDestroy(e0[r]);
+        if (e1[r]) (void)hipEventDestroy(e1[r]);
+        if (tile[r]) (void)hipFree(tile[r]);
+        if (seg[r]) (void)hipFree(seg[r]);
+        if (st[r]) (void)hipStreamDestroy(st[r]);
+        if (sc[r]) rt_scene_destroy(sc[r]);
+    }
+    (void)hipSetDevice(0);
+    for (int r = 1; r < N; ++r)
+        if (recv[r]) (void)hipFree(recv[r]);
+    if (frame) (void)hipFree(frame);
+    if (rc == RT_OK && stats) {
+        stats->primaries = static_cast<uint64_t>(W) * H * base.spp;
+        stats->segments = segs[0];
+        stats->sphere_tests = segs[1];
+        stats->box_tests = segs[2];
+        stats->kernel_ms = kms;
+        stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return rc;
 }
 
 } // extern "C"

@@ -74,7 +74,10 @@ __device__ __forceinline__ float canonical(uint64_t &st, uint64_t inc)
     float r = (float)pcg_next(st, inc) * 0x1p-32f;
     return r >= 1.f ? 0x1.fffffep-1f : r;
 }
-__device__ __forceinline__ f3 random_in_unit_sphere(uint64_t &st, uint64_t inc) // raytracer.hxx:32-43
+// raytracer.hxx:32-43. `length(p) > 1` is evaluated as `norm(p) > 1 + 2^-23`: with a
+// correctly rounded sqrt the two agree for every non-negative float (checked exhaustively,
+// tests/test_numerics_cpu.py), and the loop runs as long as its slowest lane.
+__device__ __forceinline__ f3 random_in_unit_sphere(uint64_t &st, uint64_t inc)
 {
     f3 p;
     do {
@@ -82,7 +85,7 @@ __device__ __forceinline__ f3 random_in_unit_sphere(uint64_t &st, uint64_t inc) 
         float y = canonical(st, inc) * 2.f + -1.f;
         float z = canonical(st, inc) * 2.f + -1.f;
         p = mk(x, y, z);
-    } while (length(p) > 1.f);
+    } while (p.x * p.x + p.y * p.y + p.z * p.z > 0x1.000002p+0f);
     return p;
 }
 
@@ -102,18 +105,26 @@ __device__ __forceinline__ float schlick(float ri, float c)
 }
 
 // ---- work decomposition ----------------------------------------------------------------
-__device__ __forceinline__ void pixel_of(uint32_t W, uint32_t tiled_rows, uint32_t tiles_x, uint32_t i, uint32_t &x,
-                                         uint32_t &rr)
+__device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t m, uint32_t l)
 {
+    if (l == 0) return n;
+    const uint32_t t = __umulhi(n, m);
+    return (t + ((n - t) >> 1)) >> (l - 1);
+}
+
+template <class FC>
+__device__ __forceinline__ void pixel_of(const FC &fc, uint32_t i, uint32_t &x, uint32_t &rr)
+{
+    const uint32_t W = fc.W, tiled_rows = fc.tiled_rows, tiles_x = fc.tiles_x;
     const uint32_t tiled_px = tiled_rows * W;
     if (i < tiled_px) {
         uint32_t t = i >> 6, w = i & 63u;
-        uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+        uint32_t ty = udiv(t, fc.div_tiles_x.m, fc.div_tiles_x.l), tx = t - ty * tiles_x;
         x = tx * 8u + (w & 7u);
         rr = ty * 8u + (w >> 3);
     } else {
         uint32_t j = i - tiled_px;
-        rr = j / W;
+        rr = udiv(j, fc.div_W.m, fc.div_W.l);
         x = j - rr * W;
         rr += tiled_rows;
     }
@@ -365,7 +376,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             if (!has_item && rank < avail) {
                 const uint32_t I = cnext + rank;
                 const uint32_t n_pixels = fc->n_pixels;
-                const uint32_t ls = I / n_pixels;
+                const uint32_t ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
                 pix = I - ls * n_pixels;
                 slotj = fc->slot_begin + ls;
                 has_item = true;
@@ -379,7 +390,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         // ---- start a sample on lanes that have an item but no live path -------------
         if (has_item && !alive) {
             uint32_t px, rr;
-            pixel_of(fc->W, fc->tiled_rows, fc->tiles_x, pix, px, rr);
+            pixel_of(*fc, pix, px, rr);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
             const uint32_t slot = slotj & 0xffffffu, j = slotj >> 24, g4 = fc->g4;
             const uint32_t s = slot < g4 ? slot * 4u + j : g4 * 4u + (slot - g4);
@@ -443,16 +454,19 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     const f3 albedo = mk(md.x, md.y, md.z);
                     bool scattered = true;
                     f3 nd;
-                    if (kind == 0u) {                           // lambert, raytracer.hxx:132-141
-                        const f3 r = random_in_unit_sphere(rng, inc_data);
+                    // raytracer.hxx:120-199. Lambert and metal lanes share one rejection loop and
+                    // metal and dielectric lanes one normalize (the draw order is unchanged:
+                    // reflect() consumes no draws).
+                    f3 ud = d;
+                    if (kind != 0u) ud = normalize(d);
+                    f3 r = mk(0.f, 0.f, 0.f);
+                    if (kind != 2u) r = random_in_unit_sphere(rng, inc_data);
+                    if (kind == 0u) {                           // lambert, :132-141
                         nd = ((hp + hn) + r) - hp;
-                    } else if (kind == 1u) {                    // metal, raytracer.hxx:143-156
-                        const f3 refl = reflect(normalize(d), hn);
-                        const f3 r = random_in_unit_sphere(rng, inc_data);
-                        nd = refl + r * md.w;
+                    } else if (kind == 1u) {                    // metal, :143-156
+                        nd = reflect(ud, hn) + r * md.w;
                         scattered = dot(nd, hn) > 0.f;
-                    } else {                                    // dielectric, raytracer.hxx:158-194
-                        const f3 ud = normalize(d);
+                    } else {                                    // dielectric, :158-194
                         f3 outward = mk(-hn.x, -hn.y, -hn.z);
                         float ri = md.w;
                         float cosv = dot(ud, hn);
@@ -463,7 +477,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                         }
                         const f3 refr = refract(ud, outward, ri);
                         float prob = 1.f;
-                        if (length(refr) > 0.f) prob = schlick(ri, cosv);
+                        // length(refr) > 0 <=> norm > 0 (correctly rounded sqrt; NaN -> false)
+                        if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick(ri, cosv);
                         nd = canonical(rng, inc_data) < prob ? reflect(ud, hn) : refr;
                     }
                     if (!scattered) {

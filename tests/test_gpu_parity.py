@@ -235,3 +235,15 @@ def test_fast_math_within_stated_tolerance(scene_name, W, H, spp, mode):
     assert np.isfinite(img).all()
     q = np.abs(O.epilogue_rgb8(img).astype(int) - O.epilogue_rgb8(ref).astype(int))
     assert (q <= 1).mean() >= 0.99
+
+
+@pytest.mark.parametrize("ngpu", [0, 1, 2])
+def test_render_multi_matches_single(ngpu):
+    """rt_render_multi_f32 (row tiles over the visible devices, RCCL gather when N > 1) renders
+    the same bits as one device. On a 1-GPU box every ngpu collapses to N = 1."""
+    s, m = G.scene("huge")
+    W, H, spp = 64, 37, 4  # H not divisible by 2: ragged tiles
+    single, st1 = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 5))
+    multi, stm = rt.render_multi_f32((s, m), rt.make_params(W, H, spp, 64, 5), ngpu=ngpu)
+    _bits_equal(multi, single)
+    assert stm.segments == st1.segments and stm.primaries == st1.primaries

@@ -73,6 +73,7 @@ struct rt_scene {
     uint32_t blob_units[2] = {0, 0}, n_geo[2] = {0, 0}, n_always[2] = {0, 0}, n_clusters[2] = {0, 0},
              clus_offset[2] = {0, 0};
     float clus_pad[2] = {0.f, 0.f};
+    uint32_t n_clusters_real[2] = {0, 0};
     // workspace
     float *slots = nullptr;
     size_t slots_bytes = 0;
@@ -80,7 +81,7 @@ struct rt_scene {
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;
     int cu_count = 0;
-    int occ[4][3];  // [variant][cull structure] blocks per CU, -1 = not queried
+    int occ[4][5];  // [variant][cull structure] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     size_t max_lds = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
@@ -216,7 +217,7 @@ struct scene_builder {
 // ---- scene blob: always-tested list + spatial clusters -------------------
 struct blob_t {
     std::vector<float> data;  // 16-byte units
-    uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0;
+    uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0, n_clusters_real = 0;
     float clus_pad = 0.f;
 };
 
@@ -312,6 +313,16 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     }
     b.n_geo = static_cast<uint32_t>(sidx.size());
     b.n_clusters = static_cast<uint32_t>(clusters.size());
+    b.n_clusters_real = b.n_clusters;
+    // pad to a multiple of 4 clusters (grouped box tests) with boxes no ray enters:
+    // negative extents make t_in > t_out whatever the ray
+    while (b.n_clusters % 4) {
+        uint32_t packed = static_cast<uint32_t>(sidx.size());  // count 0
+        float pf;
+        std::memcpy(&pf, &packed, 4);
+        crec.insert(crec.end(), {0.f, 0.f, 0.f, -1e30f, -1e30f, -1e30f, 0.f, pf});
+        ++b.n_clusters;
+    }
     // layout in 16-byte units: geo | sidx (padded) | clusters
     b.data = geo;
     if (b.data.empty()) b.data.assign(4, 0.f);
@@ -385,14 +396,15 @@ void fill_frame_consts(rt::KParams &k)
     f.div_n_pixels = make_udiv(k.n_pixels);
 }
 
-// Culling loop structure: 1 = box then its spheres, cluster by cluster (default, measured
-// faster); 2 = every box first into per-lane masks, then the wave walks the union of the
-// masks (RT_CULL_STRUCTURE=2 selects it for A/B; same bits).
+// Culling loop structure (RT_CULL_STRUCTURE selects one for A/B; all give the same bits):
+// 1 = box then its spheres, cluster by cluster (default); 2 = every box first into per-lane
+// masks, then the wave walks the union of the masks; 3 / 4 = boxes of 2 / 4 clusters at a
+// time (loads batched), then their spheres.
 int cull_structure()
 {
     const char *e = std::getenv("RT_CULL_STRUCTURE");
     const int v = e ? std::atoi(e) : 1;
-    return (v == 1 || v == 2) ? v : 1;
+    return (v >= 1 && v <= 4) ? v : 1;
 }
 
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
@@ -498,6 +510,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         sc->n_clusters[b] = blobs[b].n_clusters;
         sc->clus_offset[b] = blobs[b].clus_offset;
         sc->clus_pad[b] = blobs[b].clus_pad;
+        sc->n_clusters_real[b] = blobs[b].n_clusters_real;
     }
     if (rc == RT_OK) rc = up((void **)&sc->hitrec, hit.data(), hit.size() * 4);
     if (rc == RT_OK) {
@@ -600,6 +613,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.n_clusters = sc->n_clusters[b];
     k.clus_offset = sc->clus_offset[b];
     k.clus_pad = sc->clus_pad[b];
+    k.n_clusters_real = sc->n_clusters_real[b];
     const size_t lds = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(k.blob_units) * 16u;
     int &occ = sc->occ[variant][cull_mode];
     if (occ < 0) {

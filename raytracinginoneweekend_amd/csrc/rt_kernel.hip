@@ -224,22 +224,37 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float px = pad * aix, py = pad * aiy, pz = pad * aiz;
         const float tb_hi = h.t * 1.002f;
         const float t_lo = 0.5f * RT_TMIN;
-        if (CULL == 1) {  // interleaved: box, then its spheres, one cluster after another
-            for (uint32_t c = 0; c < p.n_clusters; ++c) {
-                const float4 c0 = clus[2 * c], c1 = clus[2 * c + 1];
-                const float hx = fmaf(c0.w, aix, px), hy = fmaf(c1.x, aiy, py), hz = fmaf(c1.y, aiz, pz);
-                const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
-                const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
-                const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
-                if (tin <= tout && tout >= t_lo && tin <= h.t * 1.002f) {
-                    const uint32_t sc = __builtin_amdgcn_readfirstlane(__float_as_uint(c1.w));
-                    const uint32_t start = sc & 0xffffu, cnt = sc >> 16;
-                    if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
-                    for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
-                    tests += cnt << 16;
+        if (CULL == 1 || CULL >= 3) {
+            // interleaved: boxes of G clusters (G = 1, or 2/4 with their LDS reads issued
+            // together), then each passing cluster's spheres. The box tests of a group use the
+            // t_best from before the group: older, larger, still conservative.
+            constexpr uint32_t G = CULL == 1 ? 1u : (CULL == 3 ? 2u : 4u);
+            for (uint32_t c = 0; c < p.n_clusters; c += G) {
+                bool pass[G];
+                uint32_t sc[G];
+                const float tb_now = h.t * 1.002f;
+#pragma unroll
+                for (uint32_t g = 0; g < G; ++g) {
+                    const float4 c0 = clus[2 * (c + g)], c1 = clus[2 * (c + g) + 1];
+                    const float hx = fmaf(c0.w, aix, px), hy = fmaf(c1.x, aiy, py), hz = fmaf(c1.y, aiz, pz);
+                    const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
+                    const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+                    const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+                    pass[g] = tin <= tout && tout >= t_lo && tin <= tb_now;
+                    sc[g] = __float_as_uint(c1.w);
+                }
+#pragma unroll
+                for (uint32_t g = 0; g < G; ++g) {
+                    if (pass[g]) {
+                        const uint32_t scu = __builtin_amdgcn_readfirstlane(sc[g]);
+                        const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
+                        if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
+                        for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                        tests += cnt << 16;
+                    }
                 }
             }
-            tests += p.n_clusters;
+            tests += p.n_clusters_real;
             return h;
         }
         // pass 1: every box (<= RT_MAX_CLUSTERS), masks per group of 32
@@ -266,7 +281,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
             masks[gi] = mask;
             unions[gi] = any;
         }
-        tests += p.n_clusters;
+        tests += p.n_clusters_real;
         // pass 2: the wave walks the union of the lanes' masks
 #pragma unroll
         for (uint32_t gi = 0; gi < RT_MAX_CLUSTERS / 32; ++gi) {
@@ -606,6 +621,8 @@ template <int V, bool STATS> static const void *ptr3(int cull)
 {
     if (cull == 1) return reinterpret_cast<const void *>(&render_kernel<V, 1, STATS>);
     if (cull == 2) return reinterpret_cast<const void *>(&render_kernel<V, 2, STATS>);
+    if (cull == 3) return reinterpret_cast<const void *>(&render_kernel<V, 3, STATS>);
+    if (cull == 4) return reinterpret_cast<const void *>(&render_kernel<V, 4, STATS>);
     return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS>);
 }
 

@@ -59,7 +59,15 @@ hv hnorm(hv a)
 }
 hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x}; }
 
-constexpr uint32_t kMaxSlotsBytes = 1u << 31;  // slot workspace per pass (2 GiB)
+constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 GiB)
+
+// RT_SLOT_BUDGET_BYTES lowers the per-pass slot workspace (tests force multi-pass renders).
+uint64_t slot_budget()
+{
+    const char *e = std::getenv("RT_SLOT_BUDGET_BYTES");
+    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
+    return v ? std::min<uint64_t>(v, kMaxSlotsBytes) : kMaxSlotsBytes;
+}
 
 } // namespace
 
@@ -623,7 +631,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
 
     // pass planning: the slot workspace of one pass stays under kMaxSlotsBytes
     const uint64_t per_slot = n_pixels * 12ull;
-    uint32_t slots_per_pass = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(k.n_slots, kMaxSlotsBytes / per_slot)));
+    uint32_t slots_per_pass = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(k.n_slots, slot_budget() / per_slot)));
     slots_per_pass = static_cast<uint32_t>(std::min<uint64_t>(slots_per_pass, ((1ull << 31) - 64) / n_pixels));
     if (int rc = ensure((void **)&sc->slots, &sc->slots_bytes, per_slot * slots_per_pass); rc) return rc;
     if (slots_per_pass < k.n_slots)

@@ -247,3 +247,17 @@ def test_render_multi_matches_single(ngpu):
     multi, stm = rt.render_multi_f32((s, m), rt.make_params(W, H, spp, 64, 5), ngpu=ngpu)
     _bits_equal(multi, single)
     assert stm.segments == st1.segments and stm.primaries == st1.primaries
+
+
+@pytest.mark.parametrize("spp", [9, 16])
+def test_multi_pass_slots_bit_exact(spp, monkeypatch):
+    """A slot workspace smaller than the frame's slots forces several render passes whose
+    partial sums are carried between passes; the addition order, hence the bits, must not
+    change (config 5 at 1024 spp needs two passes)."""
+    s, m = G.scene("huge")
+    W, H = 64, 32
+    one, st1 = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 3))
+    monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * 2))  # 2 slots per pass
+    many, stn = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 3))
+    _bits_equal(many, one)
+    assert stn.segments == st1.segments

@@ -405,14 +405,14 @@ void fill_frame_consts(rt::KParams &k)
 }
 
 // Culling loop structure (RT_CULL_STRUCTURE selects one for A/B; all give the same bits):
-// 1 = box then its spheres, cluster by cluster (default); 2 = every box first into per-lane
-// masks, then the wave walks the union of the masks; 3 / 4 = boxes of 2 / 4 clusters at a
-// time (loads batched), then their spheres.
+// 1 = box then its spheres, cluster by cluster; 2 = every box first into per-lane masks,
+// then the wave walks the union of the masks; 3 / 4 = boxes of 2 / 4 clusters at a time
+// (loads batched), then their spheres. Default 3 (measured fastest: 9.2 vs 9.6 ms for 1).
 int cull_structure()
 {
     const char *e = std::getenv("RT_CULL_STRUCTURE");
-    const int v = e ? std::atoi(e) : 1;
-    return (v >= 1 && v <= 4) ? v : 1;
+    const int v = e ? std::atoi(e) : 3;
+    return (v >= 1 && v <= 4) ? v : 3;
 }
 
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).

@@ -59,6 +59,7 @@ struct KParams {
     uint32_t blob_units;     // 16-byte units
     uint32_t n_geo, n_always, n_clusters, clus_offset;
     uint32_t n_clusters_real;  // n_clusters counts never-entered padding boxes (multiple of 4)
+    uint32_t n_supers, supers_offset;  // level 2: groups of 4 consecutive clusters, 2 float4 each
     float clus_pad;          // max over clusters of 1e-3 * (|C|_1 + |e|_1) + 1e-6 (per-ray pad adds 1e-3 |o|_1)
     // per-sphere hit record joined with its material, indexed by original sphere index:
     // {cx, cy, cz, r}, {albedo rgb, param}, {kind, 0, 0, 0}

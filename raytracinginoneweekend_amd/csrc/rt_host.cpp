@@ -81,7 +81,7 @@ struct rt_scene {
     uint32_t blob_units[2] = {0, 0}, n_geo[2] = {0, 0}, n_always[2] = {0, 0}, n_clusters[2] = {0, 0},
              clus_offset[2] = {0, 0};
     float clus_pad[2] = {0.f, 0.f};
-    uint32_t n_clusters_real[2] = {0, 0};
+    uint32_t n_clusters_real[2] = {0, 0}, n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     // workspace
     float *slots = nullptr;
     size_t slots_bytes = 0;
@@ -89,7 +89,7 @@ struct rt_scene {
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;
     int cu_count = 0;
-    int occ[4][5];  // [variant][cull structure] blocks per CU, -1 = not queried
+    int occ[4][6];  // [variant][cull structure] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     size_t max_lds = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
@@ -226,6 +226,7 @@ struct scene_builder {
 struct blob_t {
     std::vector<float> data;  // 16-byte units
     uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0, n_clusters_real = 0;
+    uint32_t n_supers = 0, supers_offset = 0;
     float clus_pad = 0.f;
 };
 
@@ -277,7 +278,8 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     }
     std::vector<std::vector<uint32_t>> clusters;
     if (!rest.empty()) split_clusters(s, rest, clusters);
-    std::sort(clusters.begin(), clusters.end(), [](const auto &x, const auto &y) { return x.front() < y.front(); });
+    // clusters stay in the DFS order of the median-split tree: 4 consecutive clusters are a
+    // depth-2 subtree, spatially tight, and become one level-2 box
 
     auto pad8 = [](uint32_t x) { return (x + 7u) & ~7u; };
     std::vector<float> geo;
@@ -298,6 +300,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     push(always);
     b.n_always = static_cast<uint32_t>(sidx.size());
     std::vector<float> crec;
+    std::vector<float> boxes;  // per cluster lo/hi (6 floats), for the level-2 boxes
     for (const auto &c : clusters) {
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i : c)
@@ -310,6 +313,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
             C[a] = .5f * (lo[a] + hi[a]);
             E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
         }
+        boxes.insert(boxes.end(), {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
         const float kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
         b.clus_pad = std::max(b.clus_pad, kc);
         const uint32_t start = push(c);
@@ -343,6 +347,30 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     }
     b.clus_offset = static_cast<uint32_t>(b.data.size() / 4);
     b.data.insert(b.data.end(), crec.begin(), crec.end());
+    // level 2: one box over every 4 consecutive clusters (padding clusters contribute nothing)
+    b.supers_offset = static_cast<uint32_t>(b.data.size() / 4);
+    for (uint32_t g = 0; g < b.n_clusters; g += 4) {
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t c = g; c < std::min(g + 4, b.n_clusters_real); ++c)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], boxes[6 * c + a]);
+                hi[a] = std::max(hi[a], boxes[6 * c + 3 + a]);
+            }
+        float C[3] = {0.f, 0.f, 0.f}, E[3] = {-1e30f, -1e30f, -1e30f};
+        if (g < b.n_clusters_real)
+            for (int a = 0; a < 3; ++a) {
+                C[a] = .5f * (lo[a] + hi[a]);
+                E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
+            }
+        const float kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + std::max(E[0], 0.f) +
+                                    std::max(E[1], 0.f) + std::max(E[2], 0.f)) + 1e-6f;
+        b.clus_pad = std::max(b.clus_pad, kc);
+        uint32_t packed = g | (4u << 16);
+        float pf;
+        std::memcpy(&pf, &packed, 4);
+        b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
+        ++b.n_supers;
+    }
     return b;
 }
 
@@ -407,12 +435,13 @@ void fill_frame_consts(rt::KParams &k)
 // Culling loop structure (RT_CULL_STRUCTURE selects one for A/B; all give the same bits):
 // 1 = box then its spheres, cluster by cluster; 2 = every box first into per-lane masks,
 // then the wave walks the union of the masks; 3 / 4 = boxes of 2 / 4 clusters at a time
-// (loads batched), then their spheres. Default 3 (measured fastest: 9.2 vs 9.6 ms for 1).
+// (loads batched), then their spheres; 5 = two levels: a box over each 4 clusters, then
+// structure 3 inside the passing ones. Default 5 (config 3: 8.4 ms; 3: 9.2-9.4; 1: 9.6-9.7).
 int cull_structure()
 {
     const char *e = std::getenv("RT_CULL_STRUCTURE");
-    const int v = e ? std::atoi(e) : 3;
-    return (v >= 1 && v <= 4) ? v : 3;
+    const int v = e ? std::atoi(e) : 5;
+    return (v >= 1 && v <= 5) ? v : 5;
 }
 
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
@@ -519,6 +548,8 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         sc->clus_offset[b] = blobs[b].clus_offset;
         sc->clus_pad[b] = blobs[b].clus_pad;
         sc->n_clusters_real[b] = blobs[b].n_clusters_real;
+        sc->n_supers[b] = blobs[b].n_supers;
+        sc->supers_offset[b] = blobs[b].supers_offset;
     }
     if (rc == RT_OK) rc = up((void **)&sc->hitrec, hit.data(), hit.size() * 4);
     if (rc == RT_OK) {
@@ -622,6 +653,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.clus_offset = sc->clus_offset[b];
     k.clus_pad = sc->clus_pad[b];
     k.n_clusters_real = sc->n_clusters_real[b];
+    k.n_supers = sc->n_supers[b];
+    k.supers_offset = sc->supers_offset[b];
     const size_t lds = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(k.blob_units) * 16u;
     int &occ = sc->occ[variant][cull_mode];
     if (occ < 0) {

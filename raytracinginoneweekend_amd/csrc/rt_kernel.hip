@@ -204,6 +204,18 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
 #define RT_PAD_REL 1e-3f
 #define RT_MAX_CLUSTERS 128  // rt_host.cpp sizes clusters so a scene never needs more
 
+struct RayBox {  // per-segment constants of the padded slab test
+    float ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz;
+};
+__device__ __forceinline__ bool box_pass(const RayBox &r, float4 c0, float4 c1, float t_lo, float t_hi)
+{
+    const float hx = fmaf(c0.w, r.aix, r.px), hy = fmaf(c1.x, r.aiy, r.py), hz = fmaf(c1.y, r.aiz, r.pz);
+    const float tcx = fmaf(c0.x, r.ix, -r.oix), tcy = fmaf(c0.y, r.iy, -r.oiy), tcz = fmaf(c0.z, r.iz, -r.oiz);
+    const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
+    const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
+    return tin <= tout && tout >= t_lo && tin <= t_hi;
+}
+
 template <bool FAST, int CULL, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
@@ -224,7 +236,39 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float px = pad * aix, py = pad * aiy, pz = pad * aiz;
         const float tb_hi = h.t * 1.002f;
         const float t_lo = 0.5f * RT_TMIN;
-        if (CULL == 1 || CULL >= 3) {
+        if (CULL == 5) {
+            // two levels: a box over each 4 clusters, then pairs of cluster boxes inside
+            const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
+            const float4 *sup = clus + (p.supers_offset - p.clus_offset);
+            for (uint32_t g = 0; g < p.n_supers; ++g) {
+                const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
+                ++tests;
+                if (!box_pass(rb, s0, s1, t_lo, h.t * 1.002f)) continue;
+                const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
+                tests += 4;
+                for (uint32_t c = c0i; c < c0i + 4; c += 2) {
+                    const float tb_now = h.t * 1.002f;
+                    const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
+                    const bool pa = box_pass(rb, a0, a1, t_lo, tb_now), pb = box_pass(rb, b0, b1, t_lo, tb_now);
+                    if (pa) {
+                        const uint32_t scu = __builtin_amdgcn_readfirstlane(__float_as_uint(a1.w));
+                        const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
+                        if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
+                        for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                        tests += cnt << 16;
+                    }
+                    if (pb) {
+                        const uint32_t scu = __builtin_amdgcn_readfirstlane(__float_as_uint(b1.w));
+                        const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
+                        if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
+                        for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                        tests += cnt << 16;
+                    }
+                }
+            }
+            return h;
+        }
+        if (CULL == 1 || (CULL >= 3 && CULL <= 4)) {
             // interleaved: boxes of G clusters (G = 1, or 2/4 with their LDS reads issued
             // together), then each passing cluster's spheres. The box tests of a group use the
             // t_best from before the group: older, larger, still conservative.
@@ -623,6 +667,7 @@ template <int V, bool STATS> static const void *ptr3(int cull)
     if (cull == 2) return reinterpret_cast<const void *>(&render_kernel<V, 2, STATS>);
     if (cull == 3) return reinterpret_cast<const void *>(&render_kernel<V, 3, STATS>);
     if (cull == 4) return reinterpret_cast<const void *>(&render_kernel<V, 4, STATS>);
+    if (cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS>);
     return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS>);
 }
 

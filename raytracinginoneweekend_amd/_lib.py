@@ -10,7 +10,8 @@ import os
 from . import _abi as abi
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "librt_mi355x.so")
+# RT_LIB_PATH points at another build of the same C ABI (timing ablations only)
+LIB_PATH = os.environ.get("RT_LIB_PATH") or os.path.join(PKG, "librt_mi355x.so")
 
 _lib = None
 

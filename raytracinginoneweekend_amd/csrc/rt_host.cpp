@@ -261,27 +261,36 @@ void split_clusters(const rt_sphere *s, std::vector<uint32_t> ids, std::vector<s
 
 blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
 {
-    std::vector<uint32_t> always, rest;
+    // three classes by |r| against the median: huge (> 64x, e.g. the ground) are tested on
+    // every segment; big (> 4x) and small are clustered separately so that one big sphere
+    // does not inflate the boxes of the small ones
+    std::vector<uint32_t> always, big, small;
     if (clustered && n >= 2 * kClusterMax) {
         std::vector<float> r(n);
         for (uint32_t i = 0; i < n; ++i) r[i] = std::fabs(s[i].radius);
         std::vector<float> sorted = r;
         std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
-        const float big = 4.f * sorted[n / 2];
+        const float med = sorted[n / 2];
         for (uint32_t i = 0; i < n; ++i) {
             const bool finite = std::isfinite(s[i].center[0]) && std::isfinite(s[i].center[1]) &&
                                 std::isfinite(s[i].center[2]) && std::isfinite(r[i]);
-            (finite && r[i] <= big ? rest : always).push_back(i);
+            if (!finite || r[i] > 64.f * med) always.push_back(i);
+            else if (r[i] > 4.f * med) big.push_back(i);
+            else small.push_back(i);
         }
     } else {
         for (uint32_t i = 0; i < n; ++i) always.push_back(i);
     }
+    // clusters: the big ones, padded to a multiple of 4 (an empty slot never passes), then the
+    // small ones; each group of 4 consecutive clusters gets a level-2 box
     std::vector<std::vector<uint32_t>> clusters;
-    if (!rest.empty()) split_clusters(s, rest, clusters);
+    if (!big.empty()) split_clusters(s, big, clusters);
+    while (clusters.size() % 4) clusters.emplace_back();
+    if (!small.empty()) split_clusters(s, small, clusters);
     // clusters stay in the DFS order of the median-split tree: 4 consecutive clusters are a
     // depth-2 subtree, spatially tight, and become one level-2 box
 
-    auto pad8 = [](uint32_t x) { return (x + 7u) & ~7u; };
+    auto pad4 = [](uint32_t x) { return (x + 3u) & ~3u; };
     std::vector<float> geo;
     std::vector<uint32_t> sidx;
     auto push = [&](const std::vector<uint32_t> &ids) {
@@ -290,7 +299,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
             geo.insert(geo.end(), {s[i].center[0], s[i].center[1], s[i].center[2], s[i].radius * s[i].radius}); // raytracer.hxx:58
             sidx.push_back(i);
         }
-        while (sidx.size() < base + pad8(static_cast<uint32_t>(ids.size()))) {
+        while (sidx.size() < base + pad4(static_cast<uint32_t>(ids.size()))) {
             geo.insert(geo.end(), {0.f, 0.f, 0.f, -INFINITY});  // never hits
             sidx.push_back(0xffffffffu);
         }
@@ -308,16 +317,19 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
                 lo[a] = std::min(lo[a], s[i].center[a] - std::fabs(s[i].radius));
                 hi[a] = std::max(hi[a], s[i].center[a] + std::fabs(s[i].radius));
             }
-        float C[3], E[3];
-        for (int a = 0; a < 3; ++a) {
-            C[a] = .5f * (lo[a] + hi[a]);
-            E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
+        float C[3] = {0.f, 0.f, 0.f}, E[3] = {-1e30f, -1e30f, -1e30f};  // empty: no ray enters
+        float kc = 0.f;
+        if (!c.empty()) {
+            for (int a = 0; a < 3; ++a) {
+                C[a] = .5f * (lo[a] + hi[a]);
+                E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
+            }
+            kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
+            b.clus_pad = std::max(b.clus_pad, kc);
         }
         boxes.insert(boxes.end(), {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
-        const float kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
-        b.clus_pad = std::max(b.clus_pad, kc);
         const uint32_t start = push(c);
-        const uint32_t cnt = pad8(static_cast<uint32_t>(c.size()));
+        const uint32_t cnt = pad4(static_cast<uint32_t>(c.size()));
         uint32_t packed = start | (cnt << 16);
         float pf;
         std::memcpy(&pf, &packed, 4);
@@ -357,14 +369,15 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
                 hi[a] = std::max(hi[a], boxes[6 * c + 3 + a]);
             }
         float C[3] = {0.f, 0.f, 0.f}, E[3] = {-1e30f, -1e30f, -1e30f};
-        if (g < b.n_clusters_real)
+        float kc = 0.f;
+        if (lo[0] <= hi[0]) {
             for (int a = 0; a < 3; ++a) {
                 C[a] = .5f * (lo[a] + hi[a]);
                 E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
             }
-        const float kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + std::max(E[0], 0.f) +
-                                    std::max(E[1], 0.f) + std::max(E[2], 0.f)) + 1e-6f;
-        b.clus_pad = std::max(b.clus_pad, kc);
+            kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
+            b.clus_pad = std::max(b.clus_pad, kc);
+        }
         uint32_t packed = g | (4u << 16);
         float pf;
         std::memcpy(&pf, &packed, 4);

@@ -56,6 +56,12 @@ __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta)                    
 // ---- RNG: PCG32 XSH-RR per (pixel, sample) stream; the increment is wave-uniform ---------
 __device__ __forceinline__ uint32_t pcg_next(uint64_t &state, uint64_t inc)
 {
+#ifdef RT_RNG_ABLATION  // timing-only build: xorshift32 on the low word (wrong bits by design)
+    uint32_t x = (uint32_t)state | 1u;
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    state = (state & 0xffffffff00000000ull) | x;
+    return x;
+#endif
     uint64_t old = state;
     state = old * 6364136223846793005ULL + inc;
     uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
@@ -153,13 +159,13 @@ struct Hit {
     uint32_t id;   // original sphere index, 0xffffffff = none
 };
 
-template <bool FAST, bool STATS>
+template <bool FAST, bool STATS, int N = 8>
 __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx, uint32_t i,
                                             f3 o, f3 d, float a, Hit &h, Dbg &dbg)
 {
-    float bq[8], dq[8];
+    float bq[N], dq[N];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < N; ++k) {
         const float4 s = geo[i + k];
         const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;       // raytracer.hxx:55
         if (FAST) {  // contracted: 11 VALU per sphere
@@ -174,11 +180,12 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
             dq[k] = b * b - a * c;                                           // :60
         }
     }
-    float m = fmaxf(fmaxf(fmaxf(dq[0], dq[1]), fmaxf(dq[2], dq[3])), fmaxf(fmaxf(dq[4], dq[5]), fmaxf(dq[6], dq[7])));
+    float m = fmaxf(fmaxf(dq[0], dq[1]), fmaxf(dq[2], dq[3]));
+    if (N == 8) m = fmaxf(m, fmaxf(fmaxf(dq[4 % N], dq[5 % N]), fmaxf(dq[6 % N], dq[7 % N])));
     if (m > 0.f) {
         if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < N; ++k) {
             if (dq[k] > 0.f) {                                               // :62
                 if (STATS) { ++dbg.lane_roots; if (first_active_lane()) ++dbg.wave_roots; }
                 const float q = sqrtf(dq[k]);
@@ -204,6 +211,17 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
 #define RT_PAD_REL 1e-3f
 #define RT_MAX_CLUSTERS 128  // rt_host.cpp sizes clusters so a scene never needs more
 
+// a cluster's members: blocks of 8, then one block of 4 (counts are multiples of 4)
+template <bool FAST, bool STATS>
+__device__ __forceinline__ void run_members(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
+                                            uint32_t start, uint32_t cnt, f3 o, f3 d, float a, Hit &h, Dbg &dbg)
+{
+    const uint32_t end = start + cnt;
+    uint32_t i = start;
+    for (; i + 8 <= end; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+    if (i < end) test_block8<FAST, STATS, 4>(geo, sidx, i, o, d, a, h, dbg);
+}
+
 struct RayBox {  // per-segment constants of the padded slab test
     float ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz;
 };
@@ -223,7 +241,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
 {
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
     Hit h{RT_TMAX, 0xffffffffu};
-    for (uint32_t i = 0; i < p.n_always; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+    run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, a, h, dbg);
     tests += p.n_always;
     if (CULL) {
         auto safe_rcp = [](float x) {
@@ -253,15 +271,15 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
                     if (pa) {
                         const uint32_t scu = __builtin_amdgcn_readfirstlane(__float_as_uint(a1.w));
                         const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-                        if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
-                        for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                        if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
+                        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
                         tests += cnt << 16;
                     }
                     if (pb) {
                         const uint32_t scu = __builtin_amdgcn_readfirstlane(__float_as_uint(b1.w));
                         const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-                        if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
-                        for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                        if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
+                        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
                         tests += cnt << 16;
                     }
                 }
@@ -292,8 +310,8 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
                     if (pass[g]) {
                         const uint32_t scu = __builtin_amdgcn_readfirstlane(sc[g]);
                         const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-                        if (STATS && first_active_lane()) dbg.wave_member_blocks += cnt / 8;
-                        for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                        if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
+                        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
                         tests += cnt << 16;
                     }
                 }
@@ -340,7 +358,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
                     const uint32_t sc = __float_as_uint(clus[2 * (g + c) + 1].w);
                     const uint32_t start = __builtin_amdgcn_readfirstlane(sc & 0xffffu);
                     const uint32_t cnt = __builtin_amdgcn_readfirstlane(sc >> 16);
-                    for (uint32_t i = start; i < start + cnt; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
+                    run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
                     tests += cnt << 16;
                 }
             }

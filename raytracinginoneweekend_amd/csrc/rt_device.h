@@ -12,9 +12,12 @@ namespace rt {
 //   slots: the reference averages samples with libstdc++'s blocked reduce (<numeric>:443-460):
 //     ((c0+c1)+(c2+c3)) per block of 4, blocks added in order, then the spp%4 tail one by one.
 //     Slot k < G4 = spp/4 holds the block sum of samples 4k..4k+3; slot G4+j holds tail sample
-//     4*G4+j. A work item = (slot, pixel): one lane traces its 1 or 4 samples back to back.
-//   items of one launch: slots [slot_begin, slot_end) x all pixels, item I -> slot
-//     slot_begin + I / n_pixels, pixel I % n_pixels. Chunks of 64 consecutive items are
+//     4*G4+j. A work item = (pixel, a group of up to K consecutive block slots) or (pixel, one
+//     tail slot): one lane traces the group's 4K samples (or the tail sample) back to back and
+//     writes each block's sum to its own slot, so the summation order does not depend on K.
+//   items of one launch: slots [slot_begin, slot_end) x all pixels; per pixel, n_groups block
+//     groups (slot_begin + g*K .. min(+K, block_end)) then the tail slots from tail_base.
+//     Item I -> group ls = I / n_pixels, pixel I % n_pixels. Chunks of 64 consecutive items are
 //     dealt from 8 queues (chunk c belongs to queue c % 8) by per-queue atomic counters.
 // Per-render constants used only where a sample or an item starts (the kernel re-reads them
 // from the kernarg segment at each use; see render_kernel).
@@ -29,7 +32,8 @@ struct FrameConsts {
     float lens, fW, fH;
     uint32_t corrected, W, spp;
     uint32_t inc_data_lo, inc_data_hi, inc_cam_lo, inc_cam_hi;
-    uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, g4, slot_begin, pad_;
+    uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, g4, slot_begin, kblk;
+    uint32_t n_groups, block_end, tail_base, pad_;
     UDiv div_W, div_tiles_x, div_n_pixels;
 };
 
@@ -48,6 +52,7 @@ struct KParams {
     uint32_t n_pixels, tiles_x, tiled_rows;  // tiled_rows: rows covered by 8x8 tiles (0 = untiled)
     uint32_t g4, n_slots;                   // full blocks of 4, total slots
     uint32_t slot_begin, slot_end;          // this launch's slots
+    uint32_t kblk;                          // block slots per work item (K >= 1)
     uint32_t n_items, n_chunks;
     // scene
     uint32_t n_spheres, n_materials;

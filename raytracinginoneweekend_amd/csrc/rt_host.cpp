@@ -69,6 +69,15 @@ uint64_t slot_budget()
     return v ? std::min<uint64_t>(v, kMaxSlotsBytes) : kMaxSlotsBytes;
 }
 
+// Block slots (4 samples each) a lane takes per work item; fewer, longer items mean fewer
+// refills. RT_ITEM_BLOCKS overrides for A/B (1..32); every K gives the same bits.
+uint32_t item_blocks()
+{
+    const char *e = std::getenv("RT_ITEM_BLOCKS");
+    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 0ul;
+    return v >= 1 && v <= 32 ? static_cast<uint32_t>(v) : 2u;
+}
+
 } // namespace
 
 struct rt_scene {
@@ -439,6 +448,10 @@ void fill_frame_consts(rt::KParams &k)
     f.n_pixels = k.n_pixels;
     f.g4 = k.g4;
     f.slot_begin = k.slot_begin;
+    f.kblk = k.kblk;
+    f.block_end = std::min(k.slot_end, k.g4);
+    f.n_groups = f.block_end > k.slot_begin ? (f.block_end - k.slot_begin + k.kblk - 1u) / k.kblk : 0u;
+    f.tail_base = std::max(k.slot_begin, k.g4);
     f.pad_ = 0;
     f.div_W = make_udiv(k.W);
     f.div_tiles_x = make_udiv(k.tiles_x);
@@ -633,6 +646,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.tiled_rows = tiled ? (k.num_rows / 8u) * 8u : 0u;
     k.g4 = P.spp / 4u;
     k.n_slots = k.g4 + P.spp % 4u;
+    k.kblk = item_blocks();
     k.n_spheres = sc->n_spheres;
     k.n_materials = sc->n_materials;
     k.hitrec = reinterpret_cast<const float4 *>(sc->hitrec);
@@ -690,13 +704,18 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         const uint32_t s1 = std::min(k.n_slots, s0 + slots_per_pass);
         k.slot_begin = s0;
         k.slot_end = s1;
-        k.n_items = static_cast<uint32_t>(n_pixels * (s1 - s0));
+        fill_frame_consts(k);
+        const uint32_t n_tail = s1 > k.fc.tail_base ? s1 - k.fc.tail_base : 0u;
+        const uint32_t per_pixel = k.fc.n_groups + n_tail;
+        // every item maps to a slot of this pass: the slot workspace bounds the kernel's writes
+        if (per_pixel == 0 || per_pixel > s1 - s0 || k.fc.n_groups * k.kblk < k.fc.block_end - std::min(s0, k.fc.block_end))
+            return fail(RT_ERR_INVALID, "rt_render_device: inconsistent pass plan");
+        k.n_items = static_cast<uint32_t>(n_pixels * per_pixel);
         k.n_chunks = (k.n_items + 63u) / 64u;
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_chunks + 3u) / 4u)));
         RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * sizeof(uint32_t), st));
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
-        fill_frame_consts(k);
         RT_HIP(rt::launch_render(variant, cull_mode, k, grid, st));
         if (s1 == k.n_slots) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
         rt::KAccum a{};

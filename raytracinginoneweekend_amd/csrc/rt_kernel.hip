@@ -455,7 +455,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 const uint32_t n_pixels = fc->n_pixels;
                 const uint32_t ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
                 pix = I - ls * n_pixels;
-                slotj = fc->slot_begin + ls;
+                const uint32_t ng = fc->n_groups;
+                slotj = ls < ng ? fc->slot_begin + ls * fc->kblk : fc->tail_base + (ls - ng);
                 has_item = true;
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
@@ -574,27 +575,31 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 alive = false;
                 bool item_done = false;
                 f3 outv = col;
-                const uint32_t slot = slotj & 0xffffffu, j = slotj >> 24;
+                const uint32_t slot = slotj & 0xffffffu, j = slotj >> 24, jb = j & 3u;
+                uint32_t wslot = slot;
+                bool write = false;
                 if (slot >= fc->g4) {
-                    item_done = true;
-                } else if (j == 0u) {
+                    write = item_done = true;
+                } else if (jb == 0u) {
                     pair = col;
-                } else if (j == 1u) {
+                } else if (jb == 1u) {
                     pair = pair + col;
-                } else if (j == 2u) {
+                } else if (jb == 2u) {
                     c2 = col;
                 } else {
                     outv = pair + (c2 + col);
-                    item_done = true;
+                    wslot = slot + (j >> 2);
+                    write = true;
+                    item_done = wslot + 1u == min(slot + fc->kblk, fc->block_end);
                 }
                 slotj += 1u << 24;
-                if (item_done) {
-                    float *dst = p.slots + ((size_t)(slot - fc->slot_begin) * fc->n_pixels + pix) * 3u;
+                if (write) {
+                    float *dst = p.slots + ((size_t)(wslot - fc->slot_begin) * fc->n_pixels + pix) * 3u;
                     dst[0] = outv.x;
                     dst[1] = outv.y;
                     dst[2] = outv.z;
-                    has_item = false;
                 }
+                if (item_done) has_item = false;
             }
         }
     }

@@ -30,21 +30,23 @@ ds = rt.DeviceScene(arrays)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
-variants = [v.split(":") for v in a.variants.split(",")]
-times = {f"{k}:{b}": [] for k, b in variants}
+# kind:traversal[:kN] -- traversal "cullN" sets RT_CULL_STRUCTURE=N, "kN" sets RT_ITEM_BLOCKS=N
+variants = [(v.split(":") + [""])[:3] for v in a.variants.split(",")]
+times = {":".join(x for x in v if x): [] for v in variants}
 ref = None
 segs = {}
 for r in range(a.rounds + 1):
-    for kind, trav in variants:
+    for kind, trav, kb in variants:
         if trav.startswith("cull") and len(trav) > 4:
             os.environ["RT_CULL_STRUCTURE"] = trav[4:]
+        os.environ["RT_ITEM_BLOCKS"] = kb[1:] if kb.startswith("k") else ""
         p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
                            brute_force=trav == "brute")
         seg.zero_()
         ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr())
         torch.cuda.synchronize()
         ms = ds.kernel_times(1)[0]
-        name = f"{kind}:{trav}"
+        name = ":".join(x for x in (kind, trav, kb) if x)
         if r == 0:  # warm-up round: check bits
             img = out.cpu()
             if ref is None:

@@ -261,3 +261,25 @@ def test_multi_pass_slots_bit_exact(spp, monkeypatch):
     many, stn = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 3))
     _bits_equal(many, one)
     assert stn.segments == st1.segments
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kblk,budget_slots", [(1, 0), (3, 0), (5, 0), (4, 3), (32, 0)])
+def test_item_blocks_bit_exact(kblk, budget_slots, monkeypatch):
+    """A work item may cover K consecutive 4-sample blocks of a pixel (RT_ITEM_BLOCKS); each
+    block still lands in its own slot, so any K -- with ragged last groups, spp % 4 tails and
+    multi-pass slot budgets that cut groups -- gives the bits of the oracle."""
+    s, m = G.scene("huge")
+    W, H, spp = 40, 24, 23  # 5 blocks + 3 tail samples
+    p = rt.make_params(W, H, spp, 64, 11)
+    cam = O.camera_default(W, H, abi.RT_CAMERA_REFERENCE)
+    want, want_seg = O.render_f32(s, m, cam, p)
+    monkeypatch.setenv("RT_ITEM_BLOCKS", "2")
+    base, st0 = rt.render_f32((s, m), p)
+    monkeypatch.setenv("RT_ITEM_BLOCKS", str(kblk))
+    if budget_slots:
+        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_slots))
+    got, st1 = rt.render_f32((s, m), p)
+    _bits_equal(got, want)
+    _bits_equal(base, want)
+    assert st1.segments == st0.segments == want_seg

@@ -180,6 +180,11 @@ int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n)
  * members executed, [8..12] shader-clock cycles summed over waves per loop region
  * (refill, sample start, closest hit, shading, fold). Copies them out; reset zeroes.  */
 int rt_scene_debug_counters(rt_scene *scene, uint64_t out[16], int reset);
+/* Diagnostics: per-wave records of the last instrumented render launch, out[4w .. 4w+3] for
+ * wave w of the grid = {start, exit} (100 MHz realtime clock), loop iterations, and
+ * (hardware CU id << 32 | refill rounds); at most max_waves records, *n = records written
+ * (0 without RT_DEBUG_STATS=1).                                                          */
+int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, uint32_t *n);
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,
                             void *stream);

@@ -15,10 +15,15 @@ namespace rt {
 //     4*G4+j. A work item = (pixel, a group of up to K consecutive block slots) or (pixel, one
 //     tail slot): one lane traces the group's 4K samples (or the tail sample) back to back and
 //     writes each block's sum to its own slot, so the summation order does not depend on K.
-//   items of one launch: slots [slot_begin, slot_end) x all pixels; per pixel, n_groups block
-//     groups (slot_begin + g*K .. min(+K, block_end)) then the tail slots from tail_base.
-//     Item I -> group ls = I / n_pixels, pixel I % n_pixels. Chunks of 64 consecutive items are
-//     dealt from 8 queues (chunk c belongs to queue c % 8) by per-queue atomic counters.
+//   items of one launch: slots [slot_begin, slot_end) x all pixels; per pixel, in this order,
+//     n_groups block groups (slot_begin + g*K .. min(+K, group_end)), then the split blocks
+//     [group_end, group_end + n_split4/4) one sample per item, then the tail slots from
+//     tail_base. Item I -> ls = I / n_pixels, pixel I % n_pixels. The split blocks come last so
+//     the launch drains on short items (a long item on a deep path keeps its wave, and the
+//     CU, running after the queues are dry); their 4 samples land in n_split4 extra slots
+//     after the n_local regular ones and accumulate_kernel forms ((c0+c1)+(c2+c3)) from them.
+//     Chunks of 64 consecutive items are dealt from 8 queues (chunk c belongs to queue c % 8)
+//     by per-queue atomic counters.
 // Per-render constants used only where a sample or an item starts (the kernel re-reads them
 // from the kernarg segment at each use; see render_kernel).
 // Exact unsigned division by a per-render invariant d (Granlund-Montgomery, "round-up with
@@ -33,7 +38,7 @@ struct FrameConsts {
     uint32_t corrected, W, spp;
     uint32_t inc_data_lo, inc_data_hi, inc_cam_lo, inc_cam_hi;
     uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, g4, slot_begin, kblk;
-    uint32_t n_groups, block_end, tail_base, pad_;
+    uint32_t n_groups, group_end, tail_base, n_split4, n_local, pad_[3];
     UDiv div_W, div_tiles_x, div_n_pixels;
 };
 
@@ -53,6 +58,7 @@ struct KParams {
     uint32_t g4, n_slots;                   // full blocks of 4, total slots
     uint32_t slot_begin, slot_end;          // this launch's slots
     uint32_t kblk;                          // block slots per work item (K >= 1)
+    uint32_t n_split;                       // last blocks of the pass traced one sample per item
     uint32_t n_items, n_chunks;
     // scene
     uint32_t n_spheres, n_materials;
@@ -73,18 +79,24 @@ struct KParams {
     float *slots;            // [slot_end - slot_begin][n_pixels][3]
     uint32_t *queue_ctr;     // [8]
     unsigned long long *segments;  // optional [3]: segments, sphere tests, cluster box tests
-    unsigned long long *dbg;       // [8] diagnostic counters (V_STATS_LDS only)
+    unsigned long long *dbg;       // [kDbgWords] diagnostics (V_STATS_LDS only)
 };
 
 struct KAccum {
-    const float *slots;      // [n_local_slots][n_pixels][3]
+    const float *slots;      // [n_local_slots + 4 n_split][n_pixels][3]
     float *acc;              // [n_pixels][3] running sum between passes
     float *out;              // final f32 RGB
     uint8_t *out_u8;         // optional gamma/u8 output (same layout)
     uint32_t n_pixels, n_local_slots;
+    uint32_t split_local, n_split;  // local slots [split_local, +n_split) are summed from 4 samples
     uint32_t first, last, spp;
     uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame;
 };
+
+// V_STATS_LDS diagnostics buffer: 16 counters, then {start, exit, iterations, hw id | refills}
+// per wave
+constexpr uint32_t kDbgWaves = 65536;
+constexpr size_t kDbgWords = 16 + 4 * static_cast<size_t>(kDbgWaves);
 
 enum Variant : int { V_EXACT_LDS = 0, V_EXACT_SCALAR = 1, V_FAST_LDS = 2, V_STATS_LDS = 3 };
 

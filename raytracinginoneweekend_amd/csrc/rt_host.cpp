@@ -78,6 +78,15 @@ uint32_t item_blocks()
     return v >= 1 && v <= 32 ? static_cast<uint32_t>(v) : 2u;
 }
 
+// Block slots at the end of each pass traced one sample per item (RT_SPLIT_BLOCKS, 0..64 for
+// A/B; same bits for every value).
+uint32_t split_blocks()
+{
+    const char *e = std::getenv("RT_SPLIT_BLOCKS");
+    if (!e || !*e) return 1u;
+    return static_cast<uint32_t>(std::min(std::strtoul(e, nullptr, 10), 64ul));
+}
+
 } // namespace
 
 struct rt_scene {
@@ -100,6 +109,7 @@ struct rt_scene {
     int cu_count = 0;
     int occ[4][6];  // [variant][cull structure] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
+    uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
     static constexpr uint32_t kRing = 256;
@@ -449,10 +459,15 @@ void fill_frame_consts(rt::KParams &k)
     f.g4 = k.g4;
     f.slot_begin = k.slot_begin;
     f.kblk = k.kblk;
-    f.block_end = std::min(k.slot_end, k.g4);
-    f.n_groups = f.block_end > k.slot_begin ? (f.block_end - k.slot_begin + k.kblk - 1u) / k.kblk : 0u;
+    const uint32_t block_end = std::min(k.slot_end, k.g4);
+    const uint32_t n_blocks = block_end > k.slot_begin ? block_end - k.slot_begin : 0u;
+    const uint32_t n_split = std::min(k.n_split, n_blocks);
+    f.group_end = block_end - n_split;
+    f.n_groups = f.group_end > k.slot_begin ? (f.group_end - k.slot_begin + k.kblk - 1u) / k.kblk : 0u;
+    f.n_split4 = 4u * n_split;
     f.tail_base = std::max(k.slot_begin, k.g4);
-    f.pad_ = 0;
+    f.n_local = k.slot_end - k.slot_begin;
+    f.pad_[0] = f.pad_[1] = f.pad_[2] = 0;
     f.div_W = make_udiv(k.W);
     f.div_tiles_x = make_udiv(k.tiles_x);
     f.div_n_pixels = make_udiv(k.n_pixels);
@@ -665,8 +680,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     if (variant == rt::V_EXACT_LDS && debug_stats()) {
         variant = rt::V_STATS_LDS;
         if (!sc->dbg) {
-            RT_HIP(hipMalloc((void **)&sc->dbg, 16 * sizeof(unsigned long long)));
-            RT_HIP(hipMemset(sc->dbg, 0, 16 * sizeof(unsigned long long)));
+            RT_HIP(hipMalloc((void **)&sc->dbg, rt::kDbgWords * sizeof(unsigned long long)));
+            RT_HIP(hipMemset(sc->dbg, 0, rt::kDbgWords * sizeof(unsigned long long)));
         }
         k.dbg = sc->dbg;
     }
@@ -692,8 +707,11 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     // pass planning: the slot workspace of one pass stays under kMaxSlotsBytes
     const uint64_t per_slot = n_pixels * 12ull;
     uint32_t slots_per_pass = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(k.n_slots, slot_budget() / per_slot)));
-    slots_per_pass = static_cast<uint32_t>(std::min<uint64_t>(slots_per_pass, ((1ull << 31) - 64) / n_pixels));
-    if (int rc = ensure((void **)&sc->slots, &sc->slots_bytes, per_slot * slots_per_pass); rc) return rc;
+    slots_per_pass = static_cast<uint32_t>(std::min<uint64_t>(slots_per_pass, ((1ull << 31) - 64) / (4ull * n_pixels)));
+    if (slots_per_pass == 0) return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
+    k.n_split = std::min(split_blocks(), k.g4);
+    const uint64_t slots_cap = slots_per_pass + 4ull * std::min(k.n_split, slots_per_pass);
+    if (int rc = ensure((void **)&sc->slots, &sc->slots_bytes, per_slot * slots_cap); rc) return rc;
     if (slots_per_pass < k.n_slots)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_slot); rc) return rc;
     k.slots = sc->slots;
@@ -706,9 +724,10 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         k.slot_end = s1;
         fill_frame_consts(k);
         const uint32_t n_tail = s1 > k.fc.tail_base ? s1 - k.fc.tail_base : 0u;
-        const uint32_t per_pixel = k.fc.n_groups + n_tail;
+        const uint32_t per_pixel = k.fc.n_groups + k.fc.n_split4 + n_tail;
         // every item maps to a slot of this pass: the slot workspace bounds the kernel's writes
-        if (per_pixel == 0 || per_pixel > s1 - s0 || k.fc.n_groups * k.kblk < k.fc.block_end - std::min(s0, k.fc.block_end))
+        if (per_pixel == 0 || per_pixel > 4u * (s1 - s0) || k.fc.n_local + k.fc.n_split4 > slots_cap ||
+            k.fc.n_groups * k.kblk < k.fc.group_end - std::min(s0, k.fc.group_end))
             return fail(RT_ERR_INVALID, "rt_render_device: inconsistent pass plan");
         k.n_items = static_cast<uint32_t>(n_pixels * per_pixel);
         k.n_chunks = (k.n_items + 63u) / 64u;
@@ -717,6 +736,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * sizeof(uint32_t), st));
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
         RT_HIP(rt::launch_render(variant, cull_mode, k, grid, st));
+        if (variant == rt::V_STATS_LDS) sc->dbg_waves = grid * 4u;
         if (s1 == k.n_slots) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
         rt::KAccum a{};
         a.slots = sc->slots;
@@ -725,6 +745,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         a.out_u8 = nullptr;
         a.n_pixels = k.n_pixels;
         a.n_local_slots = s1 - s0;
+        a.split_local = k.fc.group_end > s0 ? k.fc.group_end - s0 : 0u;
+        a.n_split = k.fc.n_split4 / 4u;
         a.first = s0 == 0;
         a.last = s1 == k.n_slots;
         a.spp = P.spp;
@@ -765,6 +787,19 @@ int rt_scene_debug_counters(rt_scene *sc, uint64_t out[16], int reset)
     RT_HIP(hipDeviceSynchronize());
     RT_HIP(hipMemcpy(out, sc->dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     if (reset) RT_HIP(hipMemset(sc->dbg, 0, 16 * sizeof(uint64_t)));
+    return RT_OK;
+}
+
+int rt_scene_debug_timeline(rt_scene *sc, uint64_t *out, uint32_t max_waves, uint32_t *n)
+{
+    if (!sc || !out || !n) return fail(RT_ERR_INVALID, "rt_scene_debug_timeline: null argument");
+    RT_HIP(hipSetDevice(sc->device));
+    *n = 0;
+    if (!sc->dbg) return RT_OK;
+    const uint32_t waves = std::min({max_waves, sc->dbg_waves, rt::kDbgWaves});
+    RT_HIP(hipDeviceSynchronize());
+    RT_HIP(hipMemcpy(out, sc->dbg + 16, 4 * static_cast<size_t>(waves) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    *n = waves;
     return RT_OK;
 }
 

@@ -418,6 +418,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     // STATS build only: shader-clock cycles per loop region, summed over the wave's iterations
     uint64_t cyc[5] = {0, 0, 0, 0, 0};  // refill, sample start, closest hit, shading, fold
     uint64_t t_prev = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t t_wave0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz clock
     auto stamp = [&](int r) {
         if (STATS) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -455,8 +456,11 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 const uint32_t n_pixels = fc->n_pixels;
                 const uint32_t ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
                 pix = I - ls * n_pixels;
-                const uint32_t ng = fc->n_groups;
-                slotj = ls < ng ? fc->slot_begin + ls * fc->kblk : fc->tail_base + (ls - ng);
+                const uint32_t ng = fc->n_groups, ns4 = fc->n_split4;
+                if (ls < ng) slotj = fc->slot_begin + ls * fc->kblk;
+                else if (ls - ng < ns4)  // one sample of a split block: bit 31 set, j preset
+                    slotj = (fc->group_end + ((ls - ng) >> 2)) | (((ls - ng) & 3u) << 24) | 0x80000000u;
+                else slotj = fc->tail_base + (ls - ng - ns4);
                 has_item = true;
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
@@ -470,7 +474,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             uint32_t px, rr;
             pixel_of(*fc, pix, px, rr);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
-            const uint32_t slot = slotj & 0xffffffu, j = slotj >> 24, g4 = fc->g4;
+            const uint32_t slot = slotj & 0xffffffu, j = (slotj >> 24) & 0x7fu, g4 = fc->g4;
             const uint32_t s = slot < g4 ? slot * 4u + j : g4 * 4u + (slot - g4);
             const uint64_t key = ((uint64_t)py * fc->W + px) * fc->spp + s;
             const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
@@ -575,10 +579,13 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 alive = false;
                 bool item_done = false;
                 f3 outv = col;
-                const uint32_t slot = slotj & 0xffffffu, j = slotj >> 24, jb = j & 3u;
-                uint32_t wslot = slot;
+                const uint32_t slot = slotj & 0xffffffu, j = (slotj >> 24) & 0x7fu, jb = j & 3u;
+                uint32_t wslot = slot;  // local slot index = wslot - slot_begin
                 bool write = false;
-                if (slot >= fc->g4) {
+                if (slotj >> 31) {  // split block sample: extra slot n_local + 4 (b - group_end) + j
+                    wslot = fc->slot_begin + fc->n_local + 4u * (slot - fc->group_end) + j;
+                    write = item_done = true;
+                } else if (slot >= fc->g4) {
                     write = item_done = true;
                 } else if (jb == 0u) {
                     pair = col;
@@ -590,7 +597,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     outv = pair + (c2 + col);
                     wslot = slot + (j >> 2);
                     write = true;
-                    item_done = wslot + 1u == min(slot + fc->kblk, fc->block_end);
+                    item_done = wslot + 1u == min(slot + fc->kblk, fc->group_end);
                 }
                 slotj += 1u << 24;
                 if (write) {
@@ -626,6 +633,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         }
         if (lane == 0)
             for (int i = 0; i < 5; ++i) atomicAdd(p.dbg + 8 + i, (unsigned long long)cyc[i]);
+        // wave timeline: [16 + 4w] start, [17 + 4w] exit (realtime ticks), [18 + 4w] loop iterations,
+        // [19 + 4w] hardware id << 32 | refill rounds; w = wave of the grid
+        const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if (lane == 0 && w < kDbgWaves) {
+            p.dbg[16 + 4 * w] = t_wave0;
+            p.dbg[17 + 4 * w] = __builtin_amdgcn_s_memrealtime();
+            p.dbg[18 + 4 * w] = dbg_iters;
+            p.dbg[19 + 4 * w] = ((unsigned long long)__smid() << 32) | dbg_refills;
+        }
     }
 }
 
@@ -638,8 +654,17 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
     if (k.first) acc = mk(0.f, 0.f, 0.f);
     else acc = mk(k.acc[3 * i], k.acc[3 * i + 1], k.acc[3 * i + 2]);
     for (uint32_t s = 0; s < k.n_local_slots; ++s) {
-        const float *v = k.slots + ((size_t)s * k.n_pixels + i) * 3u;
-        acc = acc + mk(v[0], v[1], v[2]);
+        if (s - k.split_local < k.n_split) {  // block traced sample by sample: main.cxx:205 order
+            f3 c[4];
+            for (uint32_t j = 0; j < 4u; ++j) {
+                const float *v = k.slots + ((size_t)(k.n_local_slots + 4u * (s - k.split_local) + j) * k.n_pixels + i) * 3u;
+                c[j] = mk(v[0], v[1], v[2]);
+            }
+            acc = acc + ((c[0] + c[1]) + (c[2] + c[3]));
+        } else {
+            const float *v = k.slots + ((size_t)s * k.n_pixels + i) * 3u;
+            acc = acc + mk(v[0], v[1], v[2]);
+        }
     }
     if (!k.last) {
         k.acc[3 * i] = acc.x; k.acc[3 * i + 1] = acc.y; k.acc[3 * i + 2] = acc.z;

@@ -30,23 +30,25 @@ ds = rt.DeviceScene(arrays)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
-# kind:traversal[:kN] -- traversal "cullN" sets RT_CULL_STRUCTURE=N, "kN" sets RT_ITEM_BLOCKS=N
-variants = [(v.split(":") + [""])[:3] for v in a.variants.split(",")]
-times = {":".join(x for x in v if x): [] for v in variants}
+# kind:traversal[:kN][:sN] -- traversal "cullN" sets RT_CULL_STRUCTURE=N, "kN" RT_ITEM_BLOCKS=N,
+# "sN" RT_SPLIT_BLOCKS=N
+variants = [(v.split(":")[0], v.split(":")[1], v.split(":")[2:]) for v in a.variants.split(",")]
+times = {":".join([k, t] + x): [] for k, t, x in variants}
 ref = None
 segs = {}
 for r in range(a.rounds + 1):
-    for kind, trav, kb in variants:
+    for kind, trav, extra in variants:
         if trav.startswith("cull") and len(trav) > 4:
             os.environ["RT_CULL_STRUCTURE"] = trav[4:]
-        os.environ["RT_ITEM_BLOCKS"] = kb[1:] if kb.startswith("k") else ""
+        os.environ["RT_ITEM_BLOCKS"] = "".join(x[1:] for x in extra if x.startswith("k"))
+        os.environ["RT_SPLIT_BLOCKS"] = "".join(x[1:] for x in extra if x.startswith("s"))
         p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
                            brute_force=trav == "brute")
         seg.zero_()
         ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr())
         torch.cuda.synchronize()
         ms = ds.kernel_times(1)[0]
-        name = ":".join(x for x in (kind, trav, kb) if x)
+        name = ":".join([kind, trav] + extra)
         if r == 0:  # warm-up round: check bits
             img = out.cpu()
             if ref is None:
@@ -60,6 +62,25 @@ for r in range(a.rounds + 1):
                   f"px<=1e-3: {(px <= 1e-3).float().mean().item()*100:.3f}%", flush=True)
             if os.environ.get("RT_DEBUG_STATS") == "1":
                 print(f"{name}: counters {ds.debug_counters()}", flush=True)
+                tl = [r for r in ds.debug_timeline() if r[1] > r[0]]
+                if tl:  # wave concurrency over the launch: how much of it is drain
+                    t0 = min(r[0] for r in tl)
+                    T = max(r[1] for r in tl) - t0
+
+                    def qs(vals, scale=1.0, nd=3):
+                        v = sorted(vals)
+                        return {f"p{int(f * 100)}": round(v[min(len(v) - 1, int(f * len(v)))] / scale, nd)
+                                for f in (0.0, 0.01, 0.1, 0.5, 0.9, 0.99, 1.0)}
+                    busy = sum(r[1] - r[0] for r in tl) / (len(tl) * T)
+                    print(f"{name}: waves={len(tl)} launch={T / 1e5:.3f}ms mean wave occupancy {busy:.3f}\n"
+                          f"  start (frac) {qs([r[0] - t0 for r in tl], T)}\n"
+                          f"  exit  (frac) {qs([r[1] - t0 for r in tl], T)}\n"
+                          f"  iterations   {qs([r[2] for r in tl], 1, 0)}\n"
+                          f"  refills      {qs([r[4] for r in tl], 1, 0)}", flush=True)
+                    late = sorted(tl, key=lambda r: -r[1])[:5]
+                    print("  latest waves (start, exit frac, iters, cu, refills):",
+                          [(round((r[0] - t0) / T, 3), round((r[1] - t0) / T, 3), r[2], r[3], r[4]) for r in late],
+                          flush=True)
         else:
             times[name].append(ms)
 res = {}

@@ -264,19 +264,24 @@ def test_multi_pass_slots_bit_exact(spp, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kblk,budget_slots", [(1, 0), (3, 0), (5, 0), (4, 3), (32, 0)])
-def test_item_blocks_bit_exact(kblk, budget_slots, monkeypatch):
-    """A work item may cover K consecutive 4-sample blocks of a pixel (RT_ITEM_BLOCKS); each
-    block still lands in its own slot, so any K -- with ragged last groups, spp % 4 tails and
-    multi-pass slot budgets that cut groups -- gives the bits of the oracle."""
+@pytest.mark.parametrize("kblk,split,budget_slots", [(1, 0, 0), (3, 0, 0), (5, 1, 0), (4, 0, 3), (32, 0, 0),
+                                                    (1, 1, 0), (2, 2, 3), (2, 5, 0), (3, 64, 2), (1, 1, 1)])
+def test_item_blocks_bit_exact(kblk, split, budget_slots, monkeypatch):
+    """A work item may cover K consecutive 4-sample blocks of a pixel (RT_ITEM_BLOCKS), and the
+    last blocks of each pass may be traced one sample per item (RT_SPLIT_BLOCKS); each block
+    sum is still formed as ((c0+c1)+(c2+c3)) and lands in its own slot, so any K and split --
+    with ragged last groups, spp % 4 tails and multi-pass slot budgets that cut groups --
+    gives the bits of the oracle."""
     s, m = G.scene("huge")
     W, H, spp = 40, 24, 23  # 5 blocks + 3 tail samples
     p = rt.make_params(W, H, spp, 64, 11)
     cam = O.camera_default(W, H, abi.RT_CAMERA_REFERENCE)
     want, want_seg = O.render_f32(s, m, cam, p)
     monkeypatch.setenv("RT_ITEM_BLOCKS", "2")
+    monkeypatch.setenv("RT_SPLIT_BLOCKS", "0")
     base, st0 = rt.render_f32((s, m), p)
     monkeypatch.setenv("RT_ITEM_BLOCKS", str(kblk))
+    monkeypatch.setenv("RT_SPLIT_BLOCKS", str(split))
     if budget_slots:
         monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_slots))
     got, st1 = rt.render_f32((s, m), p)

@@ -9,21 +9,16 @@ namespace rt {
 // Work decomposition:
 //   pixel enumeration i in [0, n_pixels): the rows of this render (y = row_offset + rr*row_stride),
 //     in 8x8 tiles while both W and the row count allow, row-major for the remainder;
-//   slots: the reference averages samples with libstdc++'s blocked reduce (<numeric>:443-460):
-//     ((c0+c1)+(c2+c3)) per block of 4, blocks added in order, then the spp%4 tail one by one.
-//     Slot k < G4 = spp/4 holds the block sum of samples 4k..4k+3; slot G4+j holds tail sample
-//     4*G4+j. A work item = (pixel, a group of up to K consecutive block slots) or (pixel, one
-//     tail slot): one lane traces the group's 4K samples (or the tail sample) back to back and
-//     writes each block's sum to its own slot, so the summation order does not depend on K.
-//   items of one launch: slots [slot_begin, slot_end) x all pixels; per pixel, in this order,
-//     n_groups block groups (slot_begin + g*K .. min(+K, group_end)), then the split blocks
-//     [group_end, group_end + n_split4/4) one sample per item, then the tail slots from
-//     tail_base. Item I -> ls = I / n_pixels, pixel I % n_pixels. The split blocks come last so
-//     the launch drains on short items (a long item on a deep path keeps its wave, and the
-//     CU, running after the queues are dry); their 4 samples land in n_split4 extra slots
-//     after the n_local regular ones and accumulate_kernel forms ((c0+c1)+(c2+c3)) from them.
-//     Chunks of 64 consecutive items are dealt from 8 queues (chunk c belongs to queue c % 8)
-//     by per-queue atomic counters.
+//   a work item is one sample of one pixel: a lane traces it and stores its colour to the
+//     sample's slot [s - sample_begin][i]. The reference averages samples with libstdc++'s
+//     blocked reduce (<numeric>:443-460), ((c0+c1)+(c2+c3)) per block of 4, blocks in order,
+//     then the spp%4 tail one by one; accumulate_kernel replays that order over the slots.
+//     One-sample items keep every lane's unit of work short, so the launch drains evenly
+//     (a multi-sample item on a deep path holds its wave long after the queues are dry).
+//   items of one launch (a "pass"): samples [sample_begin, sample_end) x all pixels, item I ->
+//     sample sample_begin + I / n_pixels, pixel I % n_pixels; passes start on multiples of 4.
+//     Chunks of chunk_items consecutive items are dealt from 8 queues (chunk c belongs to
+//     queue c % 8) by per-queue atomic counters.
 // Per-render constants used only where a sample or an item starts (the kernel re-reads them
 // from the kernarg segment at each use; see render_kernel).
 // Exact unsigned division by a per-render invariant d (Granlund-Montgomery, "round-up with
@@ -37,8 +32,7 @@ struct FrameConsts {
     float lens, fW, fH;
     uint32_t corrected, W, spp;
     uint32_t inc_data_lo, inc_data_hi, inc_cam_lo, inc_cam_hi;
-    uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, g4, slot_begin, kblk;
-    uint32_t n_groups, group_end, tail_base, n_split4, n_local, pad_[3];
+    uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, sample_begin;
     UDiv div_W, div_tiles_x, div_n_pixels;
 };
 
@@ -55,11 +49,8 @@ struct KParams {
     uint64_t inc_data, inc_cam;  // PCG increments: ((2*seed) << 1) | 1 and ((2*seed+1) << 1) | 1
     // decomposition
     uint32_t n_pixels, tiles_x, tiled_rows;  // tiled_rows: rows covered by 8x8 tiles (0 = untiled)
-    uint32_t g4, n_slots;                   // full blocks of 4, total slots
-    uint32_t slot_begin, slot_end;          // this launch's slots
-    uint32_t kblk;                          // block slots per work item (K >= 1)
-    uint32_t n_split;                       // last blocks of the pass traced one sample per item
-    uint32_t n_items, n_chunks;
+    uint32_t sample_begin, sample_end;      // this launch's samples
+    uint32_t n_items, n_chunks, chunk_items;  // items dealt per queue grab (multiple of 64)
     // scene
     uint32_t n_spheres, n_materials;
     // scene blob, staged whole into LDS: [geo: n_geo float4 {cx, cy, cz, fl(r*r)}]
@@ -72,26 +63,31 @@ struct KParams {
     uint32_t n_clusters_real;  // n_clusters counts never-entered padding boxes (multiple of 4)
     uint32_t n_supers, supers_offset;  // level 2: groups of 4 consecutive clusters, 2 float4 each
     float clus_pad;          // max over clusters of 1e-3 * (|C|_1 + |e|_1) + 1e-6 (per-ray pad adds 1e-3 |o|_1)
-    // per-sphere hit record joined with its material, indexed by original sphere index:
-    // {cx, cy, cz, r}, {albedo rgb, param}, {kind, 0, 0, 0}
-    const float4 *hitrec;
+    // shading records in the blob at shade_offset, indexed by original sphere index:
+    // {cx, cy, cz, r}, {albedo rgb, param} x n_spheres, then n_spheres kind bytes (16-B padded)
+    uint32_t shade_offset;
+    uint32_t lds_units;      // blob units staged in LDS: all of it, or the part before shade_offset
+    uint32_t shade_lds;      // 1: shading records read from LDS, 0: from the global blob
     // outputs / workspace
-    float *slots;            // [slot_end - slot_begin][n_pixels][3]
-    uint32_t *queue_ctr;     // [8]
+    float *slots;            // [sample_end - sample_begin][n_pixels][3]
+    uint32_t *queue_ctr;     // [8 x kQueueStride]: one counter per 256-B line
     unsigned long long *segments;  // optional [3]: segments, sphere tests, cluster box tests
     unsigned long long *dbg;       // [kDbgWords] diagnostics (V_STATS_LDS only)
 };
 
 struct KAccum {
-    const float *slots;      // [n_local_slots + 4 n_split][n_pixels][3]
+    const float *slots;      // [n_samples][n_pixels][3], first sample a multiple of 4
     float *acc;              // [n_pixels][3] running sum between passes
     float *out;              // final f32 RGB
     uint8_t *out_u8;         // optional gamma/u8 output (same layout)
-    uint32_t n_pixels, n_local_slots;
-    uint32_t split_local, n_split;  // local slots [split_local, +n_split) are summed from 4 samples
+    uint32_t n_pixels, n_samples;
+    uint32_t n_blocks;       // full blocks of 4 among this pass's samples (the rest is the tail)
     uint32_t first, last, spp;
     uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame;
 };
+
+// queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise
+constexpr uint32_t kQueueStride = 64;
 
 // V_STATS_LDS diagnostics buffer: 16 counters, then {start, exit, iterations, hw id | refills}
 // per wave

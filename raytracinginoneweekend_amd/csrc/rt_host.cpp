@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -69,22 +70,13 @@ uint64_t slot_budget()
     return v ? std::min<uint64_t>(v, kMaxSlotsBytes) : kMaxSlotsBytes;
 }
 
-// Block slots (4 samples each) a lane takes per work item; fewer, longer items mean fewer
-// refills. RT_ITEM_BLOCKS overrides for A/B (1..32); every K gives the same bits.
-uint32_t item_blocks()
+// Items per queue grab (RT_CHUNK_ITEMS for A/B: a multiple of 64 in [64, 8192]); bigger
+// chunks mean fewer cross-XCD atomics, smaller ones a finer end-of-launch balance.
+uint32_t chunk_items()
 {
-    const char *e = std::getenv("RT_ITEM_BLOCKS");
+    const char *e = std::getenv("RT_CHUNK_ITEMS");
     const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 0ul;
-    return v >= 1 && v <= 32 ? static_cast<uint32_t>(v) : 2u;
-}
-
-// Block slots at the end of each pass traced one sample per item (RT_SPLIT_BLOCKS, 0..64 for
-// A/B; same bits for every value).
-uint32_t split_blocks()
-{
-    const char *e = std::getenv("RT_SPLIT_BLOCKS");
-    if (!e || !*e) return 1u;
-    return static_cast<uint32_t>(std::min(std::strtoul(e, nullptr, 10), 64ul));
+    return v >= 64 && v <= 8192 && v % 64 == 0 ? static_cast<uint32_t>(v) : 512u;
 }
 
 } // namespace
@@ -92,7 +84,6 @@ uint32_t split_blocks()
 struct rt_scene {
     int device = 0;
     uint32_t n_spheres = 0, n_materials = 0;
-    float *hitrec = nullptr;  // [n][3] float4: {c, r}, {albedo, param}, {kind}
     // scene blobs: [0] every sphere in index order (brute force), [1] big
     // spheres always tested + spatial clusters
     float *blob[2] = {nullptr, nullptr};
@@ -100,6 +91,7 @@ struct rt_scene {
              clus_offset[2] = {0, 0};
     float clus_pad[2] = {0.f, 0.f};
     uint32_t n_clusters_real[2] = {0, 0}, n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
+    uint32_t shade_offset[2] = {0, 0};
     // workspace
     float *slots = nullptr;
     size_t slots_bytes = 0;
@@ -107,7 +99,7 @@ struct rt_scene {
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;
     int cu_count = 0;
-    int occ[4][6];  // [variant][cull structure] blocks per CU, -1 = not queried
+    int occ[4][6][2];  // [variant][cull structure][shade records in LDS] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
@@ -245,7 +237,7 @@ struct scene_builder {
 struct blob_t {
     std::vector<float> data;  // 16-byte units
     uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0, n_clusters_real = 0;
-    uint32_t n_supers = 0, supers_offset = 0;
+    uint32_t n_supers = 0, supers_offset = 0, shade_offset = 0;
     float clus_pad = 0.f;
 };
 
@@ -456,18 +448,7 @@ void fill_frame_consts(rt::KParams &k)
     f.tiled_rows = k.tiled_rows;
     f.tiles_x = k.tiles_x;
     f.n_pixels = k.n_pixels;
-    f.g4 = k.g4;
-    f.slot_begin = k.slot_begin;
-    f.kblk = k.kblk;
-    const uint32_t block_end = std::min(k.slot_end, k.g4);
-    const uint32_t n_blocks = block_end > k.slot_begin ? block_end - k.slot_begin : 0u;
-    const uint32_t n_split = std::min(k.n_split, n_blocks);
-    f.group_end = block_end - n_split;
-    f.n_groups = f.group_end > k.slot_begin ? (f.group_end - k.slot_begin + k.kblk - 1u) / k.kblk : 0u;
-    f.n_split4 = 4u * n_split;
-    f.tail_base = std::max(k.slot_begin, k.g4);
-    f.n_local = k.slot_end - k.slot_begin;
-    f.pad_[0] = f.pad_[1] = f.pad_[2] = 0;
+    f.sample_begin = k.sample_begin;
     f.div_W = make_udiv(k.W);
     f.div_tiles_x = make_udiv(k.tiles_x);
     f.div_n_pixels = make_udiv(k.n_pixels);
@@ -489,6 +470,20 @@ int cull_structure()
 bool debug_stats()
 {
     const char *e = std::getenv("RT_DEBUG_STATS");
+    return e && e[0] == '1';
+}
+
+// RT_SHADE_LDS=0/1 forces the shading records out of / into LDS (-1 = automatic).
+int shade_lds_env()
+{
+    const char *e = std::getenv("RT_SHADE_LDS");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+}
+
+// RT_VERBOSE=1 prints each launch's plan (variant, LDS bytes, occupancy, grid, items) to stderr.
+bool verbose()
+{
+    const char *e = std::getenv("RT_VERBOSE");
     return e && e[0] == '1';
 }
 
@@ -534,7 +529,7 @@ int rt_scene_destroy(rt_scene *sc)
     (void)hipSetDevice(sc->device);
     for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
     for (auto e : sc->ev_end) (void)hipEventDestroy(e);
-    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->hitrec, (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
+    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
     delete sc;
@@ -569,8 +564,19 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         std::memcpy(h + 8, &mt.kind, 4);
     }
     blob_t blobs[2] = {build_blob(spheres, n_spheres, false), build_blob(spheres, n_spheres, true)};
+    // shading records join each blob (so they sit in LDS next to the geometry): per original
+    // sphere index {c, r}, {albedo, param}, then the material kinds as bytes, 16-B padded
+    for (blob_t &b : blobs) {
+        b.shade_offset = static_cast<uint32_t>(b.data.size() / 4);
+        for (uint32_t i = 0; i < n_spheres; ++i) b.data.insert(b.data.end(), hit.data() + 12 * static_cast<size_t>(i), hit.data() + 12 * static_cast<size_t>(i) + 8);
+        std::vector<uint8_t> kinds((n_spheres + 15u) / 16u * 16u, 0);
+        for (uint32_t i = 0; i < n_spheres; ++i) kinds[i] = static_cast<uint8_t>(materials[spheres[i].material].kind);
+        const size_t at = b.data.size();
+        b.data.resize(at + kinds.size() / 4);
+        std::memcpy(b.data.data() + at, kinds.data(), kinds.size());
+    }
     rt_scene *sc = new rt_scene();
-    for (auto &r : sc->occ) for (auto &x : r) x = -1;
+    for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
     sc->device = device;
     sc->n_spheres = n_spheres;
     sc->n_materials = n_materials;
@@ -591,10 +597,10 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         sc->n_clusters_real[b] = blobs[b].n_clusters_real;
         sc->n_supers[b] = blobs[b].n_supers;
         sc->supers_offset[b] = blobs[b].supers_offset;
+        sc->shade_offset[b] = blobs[b].shade_offset;
     }
-    if (rc == RT_OK) rc = up((void **)&sc->hitrec, hit.data(), hit.size() * 4);
     if (rc == RT_OK) {
-        hipError_t e = hipMalloc((void **)&sc->queue_ctr, 8 * sizeof(uint32_t));
+        hipError_t e = hipMalloc((void **)&sc->queue_ctr, 8 * rt::kQueueStride * sizeof(uint32_t));
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
     }
     if (rc == RT_OK) {
@@ -659,12 +665,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     const bool tiled = (P.width % 8u) == 0u;
     k.tiles_x = tiled ? P.width / 8u : 1u;
     k.tiled_rows = tiled ? (k.num_rows / 8u) * 8u : 0u;
-    k.g4 = P.spp / 4u;
-    k.n_slots = k.g4 + P.spp % 4u;
-    k.kblk = item_blocks();
     k.n_spheres = sc->n_spheres;
     k.n_materials = sc->n_materials;
-    k.hitrec = reinterpret_cast<const float4 *>(sc->hitrec);
     k.queue_ctr = sc->queue_ctr;
     k.segments = reinterpret_cast<unsigned long long *>(d_segments);
 
@@ -673,7 +675,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     int variant = (P.flags & RT_FLAG_FAST_MATH) ? rt::V_FAST_LDS : rt::V_EXACT_LDS;
     bool cull = !(P.flags & RT_FLAG_BRUTE_FORCE) && sc->n_clusters[1] > 0;
     if (P.flags & RT_FLAG_SCALAR_SCENE) { variant = rt::V_EXACT_SCALAR; cull = false; }
-    if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->blob_units[cull]) * 16u > sc->max_lds) {
+    if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->shade_offset[cull]) * 16u > sc->max_lds) {
         if (variant == rt::V_FAST_LDS || cull) return fail(RT_ERR_UNSUPPORTED, "rt_render_device: scene too large for LDS");
         variant = rt::V_EXACT_SCALAR;
     }
@@ -697,58 +699,74 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.n_clusters_real = sc->n_clusters_real[b];
     k.n_supers = sc->n_supers[b];
     k.supers_offset = sc->supers_offset[b];
-    const size_t lds = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(k.blob_units) * 16u;
-    int &occ = sc->occ[variant][cull_mode];
-    if (occ < 0) {
-        RT_HIP(rt::occupancy_render(variant, cull_mode, &occ, lds));
-        occ = std::max(occ, 1);
-    }
+    k.shade_offset = sc->shade_offset[b];
+    // the shading records (the blob's tail) join the geometry in LDS unless that costs
+    // workgroups per CU; RT_SHADE_LDS=0/1 forces the choice for A/B
+    auto occ_for = [&](int in_lds, int *out) -> int {
+        int &o = sc->occ[variant][cull_mode][in_lds];
+        if (o < 0) {
+            const size_t bytes = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(in_lds ? k.blob_units : k.shade_offset) * 16u;
+            RT_HIP(rt::occupancy_render(variant, cull_mode, &o, bytes));
+            o = std::max(o, 1);
+        }
+        *out = o;
+        return RT_OK;
+    };
+    int occ_geo = 0, occ_all = 0;
+    if (int rc = occ_for(0, &occ_geo); rc) return rc;
+    if (int rc = occ_for(1, &occ_all); rc) return rc;
+    const int force = shade_lds_env();
+    k.shade_lds = variant != rt::V_EXACT_SCALAR && static_cast<size_t>(k.blob_units) * 16u <= sc->max_lds &&
+                  (force >= 0 ? force == 1 : occ_all >= occ_geo);
+    k.lds_units = variant == rt::V_EXACT_SCALAR ? 0u : (k.shade_lds ? k.blob_units : k.shade_offset);
+    const size_t lds = static_cast<size_t>(k.lds_units) * 16u;
+    const int occ = k.shade_lds ? occ_all : occ_geo;
 
-    // pass planning: the slot workspace of one pass stays under kMaxSlotsBytes
-    const uint64_t per_slot = n_pixels * 12ull;
-    uint32_t slots_per_pass = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(k.n_slots, slot_budget() / per_slot)));
-    slots_per_pass = static_cast<uint32_t>(std::min<uint64_t>(slots_per_pass, ((1ull << 31) - 64) / (4ull * n_pixels)));
-    if (slots_per_pass == 0) return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
-    k.n_split = std::min(split_blocks(), k.g4);
-    const uint64_t slots_cap = slots_per_pass + 4ull * std::min(k.n_split, slots_per_pass);
-    if (int rc = ensure((void **)&sc->slots, &sc->slots_bytes, per_slot * slots_cap); rc) return rc;
-    if (slots_per_pass < k.n_slots)
-        if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_slot); rc) return rc;
+    // pass planning: the slot workspace of one pass (12 B per sample and pixel) stays under
+    // the budget; passes hold a multiple of 4 samples so no reduce block straddles two
+    const uint64_t per_sample = n_pixels * 12ull;
+    uint64_t spp_pass = std::min<uint64_t>(P.spp, slot_budget() / per_sample);
+    spp_pass = std::min<uint64_t>(spp_pass, ((1ull << 31) - 8192) / n_pixels);  // items fit 31 bits
+    if (spp_pass < P.spp) spp_pass &= ~3ull;
+    if (spp_pass == 0) spp_pass = 4;
+    if (n_pixels * std::min<uint64_t>(spp_pass, P.spp) >= (1ull << 31) - 8192)
+        return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
+    if (int rc = ensure((void **)&sc->slots, &sc->slots_bytes, per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc) return rc;
+    if (spp_pass < P.spp)
+        if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
     k.slots = sc->slots;
+    k.chunk_items = chunk_items();
 
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
-    for (uint32_t s0 = 0; s0 < k.n_slots; s0 += slots_per_pass) {
-        const uint32_t s1 = std::min(k.n_slots, s0 + slots_per_pass);
-        k.slot_begin = s0;
-        k.slot_end = s1;
+    const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
+    for (uint32_t s0 = 0; s0 < P.spp; s0 += static_cast<uint32_t>(spp_pass)) {
+        const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
+        k.sample_begin = s0;
+        k.sample_end = s1;
         fill_frame_consts(k);
-        const uint32_t n_tail = s1 > k.fc.tail_base ? s1 - k.fc.tail_base : 0u;
-        const uint32_t per_pixel = k.fc.n_groups + k.fc.n_split4 + n_tail;
-        // every item maps to a slot of this pass: the slot workspace bounds the kernel's writes
-        if (per_pixel == 0 || per_pixel > 4u * (s1 - s0) || k.fc.n_local + k.fc.n_split4 > slots_cap ||
-            k.fc.n_groups * k.kblk < k.fc.group_end - std::min(s0, k.fc.group_end))
-            return fail(RT_ERR_INVALID, "rt_render_device: inconsistent pass plan");
-        k.n_items = static_cast<uint32_t>(n_pixels * per_pixel);
-        k.n_chunks = (k.n_items + 63u) / 64u;
+        k.n_items = static_cast<uint32_t>(n_pixels * (s1 - s0));
+        k.n_chunks = (k.n_items + k.chunk_items - 1u) / k.chunk_items;
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_chunks + 3u) / 4u)));
-        RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * sizeof(uint32_t), st));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_items + 255u) / 256u)));
+        RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), st));
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
+        if (verbose())
+            std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) chunk=%u\n",
+                         variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1, k.chunk_items);
         RT_HIP(rt::launch_render(variant, cull_mode, k, grid, st));
         if (variant == rt::V_STATS_LDS) sc->dbg_waves = grid * 4u;
-        if (s1 == k.n_slots) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
+        if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
         rt::KAccum a{};
         a.slots = sc->slots;
         a.acc = sc->acc;
         a.out = d_rgb;
         a.out_u8 = nullptr;
         a.n_pixels = k.n_pixels;
-        a.n_local_slots = s1 - s0;
-        a.split_local = k.fc.group_end > s0 ? k.fc.group_end - s0 : 0u;
-        a.n_split = k.fc.n_split4 / 4u;
+        a.n_samples = s1 - s0;
+        a.n_blocks = (std::min(s1, full_blocks_end) - std::min(s0, full_blocks_end)) / 4u;
         a.first = s0 == 0;
-        a.last = s1 == k.n_slots;
+        a.last = s1 == P.spp;
         a.spp = P.spp;
         a.W = P.width;
         a.tiles_x = k.tiles_x;

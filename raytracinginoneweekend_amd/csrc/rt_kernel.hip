@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     if constexpr (V == V_EXACT_SCALAR) {
         blob = p.blob;
     } else {
-        for (uint32_t i = threadIdx.x; i < p.blob_units; i += blockDim.x) lds_blob[i] = p.blob[i];
+        for (uint32_t i = threadIdx.x; i < p.lds_units; i += blockDim.x) lds_blob[i] = p.blob[i];
         __syncthreads();
         blob = lds_blob;
     }
@@ -405,11 +405,10 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     uint32_t cnext = 0, cend = 0;
     bool exhausted = false;
 
-    // lane state
-    bool has_item = false, alive = false;
-    // item: pixel enumeration index + slot (low 24 bits) | sample-within-item j (bits 24-26)
-    uint32_t pix = 0, slotj = 0;
-    f3 o = mk(0.f, 0.f, 0.f), d = o, att = o, pair = o, c2 = o;
+    // lane state: the lane's item is one sample (pixel enumeration index, sample of the pass)
+    bool alive = false;
+    uint32_t pix = 0, ls = 0;
+    f3 o = mk(0.f, 0.f, 0.f), d = o, att = o;
     uint32_t depth = 0;
     uint64_t rng = 0;
     uint32_t segs = 0, tests_sph = 0, tests_box = 0;  // per-lane tallies (widened at the end)
@@ -431,13 +430,14 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         stamp(4);
         fc_ptr_t fc = fc_base;
         asm volatile("" : "+s"(fc));
-        // ---- refill items for idle lanes -------------------------------------------
-        uint64_t need = __ballot(!has_item);
+        // ---- refill items for idle lanes and start their samples -------------------
+        uint64_t need = __ballot(!alive);
+        bool fresh = false;
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
             if (cnext >= cend) {
                 uint32_t c = 0;
-                if (lane == 0) c = atomicAdd(p.queue_ctr + q, 1u);
+                if (lane == 0) c = atomicAdd(p.queue_ctr + q * kQueueStride, 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
                 const uint64_t chunk = (uint64_t)q + 8ull * c;
                 if (chunk >= p.n_chunks) {
@@ -445,37 +445,30 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     if (++q_tried == 8u) exhausted = true;
                     continue;
                 }
-                cnext = (uint32_t)chunk * 64u;
-                cend = min(cnext + 64u, p.n_items);
+                cnext = (uint32_t)chunk * p.chunk_items;
+                cend = min(cnext + p.chunk_items, p.n_items);
             }
             const uint32_t avail = cend - cnext;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            if (!has_item && rank < avail) {
+            if (!alive && rank < avail) {
                 const uint32_t I = cnext + rank;
-                const uint32_t n_pixels = fc->n_pixels;
-                const uint32_t ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
-                pix = I - ls * n_pixels;
-                const uint32_t ng = fc->n_groups, ns4 = fc->n_split4;
-                if (ls < ng) slotj = fc->slot_begin + ls * fc->kblk;
-                else if (ls - ng < ns4)  // one sample of a split block: bit 31 set, j preset
-                    slotj = (fc->group_end + ((ls - ng) >> 2)) | (((ls - ng) & 3u) << 24) | 0x80000000u;
-                else slotj = fc->tail_base + (ls - ng - ns4);
-                has_item = true;
+                ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
+                pix = I - ls * fc->n_pixels;
+                alive = fresh = true;
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
             cnext += took;
-            need = __ballot(!has_item);
+            need = __ballot(!alive);
         }
 
         stamp(0);
-        // ---- start a sample on lanes that have an item but no live path -------------
-        if (has_item && !alive) {
+        // ---- start the sample of a freshly assigned item -----------------------------
+        if (fresh) {
             uint32_t px, rr;
             pixel_of(*fc, pix, px, rr);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
-            const uint32_t slot = slotj & 0xffffffu, j = (slotj >> 24) & 0x7fu, g4 = fc->g4;
-            const uint32_t s = slot < g4 ? slot * 4u + j : g4 * 4u + (slot - g4);
+            const uint32_t s = fc->sample_begin + ls;
             const uint64_t key = ((uint64_t)py * fc->W + px) * fc->spp + s;
             const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
             const uint64_t inc_cam = ((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo;
@@ -497,7 +490,6 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             if (fc->corrected) d = d - org;
             att = mk(1.f, 1.f, 1.f);
             depth = 0;
-            alive = true;
         }
         stamp(1);
         if (__ballot(alive) == 0) break;  // only when the item space is exhausted
@@ -526,12 +518,22 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     col = bg * att;
                     done = true;
                 } else {
-                    const float4 sf = p.hitrec[3 * ib];
+                    float4 sf, md;
+                    uint32_t kind;
+                    if (V != V_EXACT_SCALAR && p.shade_lds) {
+                        const float4 *shade = blob + p.shade_offset;
+                        sf = shade[2 * ib];
+                        md = shade[2 * ib + 1];
+                        kind = reinterpret_cast<const uint8_t *>(shade + 2 * p.n_spheres)[ib];
+                    } else {
+                        const float4 *shade = p.blob + p.shade_offset;
+                        sf = shade[2 * ib];
+                        md = shade[2 * ib + 1];
+                        kind = reinterpret_cast<const uint8_t *>(shade + 2 * p.n_spheres)[ib];
+                    }
                     const f3 ctr = mk(sf.x, sf.y, sf.z);
                     const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
                     const f3 hn = (hp - ctr) / sf.w;            // raytracer.hxx:71
-                    const float4 md = p.hitrec[3 * ib + 1];     // material of the sphere
-                    const uint32_t kind = __float_as_uint(p.hitrec[3 * ib + 2].x);
                     const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
                     const f3 albedo = mk(md.x, md.y, md.z);
                     bool scattered = true;
@@ -575,38 +577,13 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             }
             stamp(3);
             if (done) {
-                // fold the finished sample into its item (main.cxx:205 blocked reduce)
+                // the sample's colour goes to its slot; accumulate_kernel forms the reference's
+                // blocked sum over the slots (main.cxx:205)
                 alive = false;
-                bool item_done = false;
-                f3 outv = col;
-                const uint32_t slot = slotj & 0xffffffu, j = (slotj >> 24) & 0x7fu, jb = j & 3u;
-                uint32_t wslot = slot;  // local slot index = wslot - slot_begin
-                bool write = false;
-                if (slotj >> 31) {  // split block sample: extra slot n_local + 4 (b - group_end) + j
-                    wslot = fc->slot_begin + fc->n_local + 4u * (slot - fc->group_end) + j;
-                    write = item_done = true;
-                } else if (slot >= fc->g4) {
-                    write = item_done = true;
-                } else if (jb == 0u) {
-                    pair = col;
-                } else if (jb == 1u) {
-                    pair = pair + col;
-                } else if (jb == 2u) {
-                    c2 = col;
-                } else {
-                    outv = pair + (c2 + col);
-                    wslot = slot + (j >> 2);
-                    write = true;
-                    item_done = wslot + 1u == min(slot + fc->kblk, fc->group_end);
-                }
-                slotj += 1u << 24;
-                if (write) {
-                    float *dst = p.slots + ((size_t)(wslot - fc->slot_begin) * fc->n_pixels + pix) * 3u;
-                    dst[0] = outv.x;
-                    dst[1] = outv.y;
-                    dst[2] = outv.z;
-                }
-                if (item_done) has_item = false;
+                float *dst = p.slots + ((size_t)ls * fc->n_pixels + pix) * 3u;
+                dst[0] = col.x;
+                dst[1] = col.y;
+                dst[2] = col.z;
             }
         }
     }
@@ -653,19 +630,15 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
     f3 acc;
     if (k.first) acc = mk(0.f, 0.f, 0.f);
     else acc = mk(k.acc[3 * i], k.acc[3 * i + 1], k.acc[3 * i + 2]);
-    for (uint32_t s = 0; s < k.n_local_slots; ++s) {
-        if (s - k.split_local < k.n_split) {  // block traced sample by sample: main.cxx:205 order
-            f3 c[4];
-            for (uint32_t j = 0; j < 4u; ++j) {
-                const float *v = k.slots + ((size_t)(k.n_local_slots + 4u * (s - k.split_local) + j) * k.n_pixels + i) * 3u;
-                c[j] = mk(v[0], v[1], v[2]);
-            }
-            acc = acc + ((c[0] + c[1]) + (c[2] + c[3]));
-        } else {
-            const float *v = k.slots + ((size_t)s * k.n_pixels + i) * 3u;
-            acc = acc + mk(v[0], v[1], v[2]);
-        }
-    }
+    // main.cxx:205 = libstdc++ reduce (<numeric>:443-460): ((c0+c1)+(c2+c3)) per block of 4,
+    // blocks in order, then the spp % 4 tail one by one. Passes start on a multiple of 4.
+    auto ld = [&](uint32_t s) {
+        const float *v = k.slots + ((size_t)s * k.n_pixels + i) * 3u;
+        return mk(v[0], v[1], v[2]);
+    };
+    uint32_t s = 0;
+    for (; s < 4u * k.n_blocks; s += 4u) acc = acc + ((ld(s) + ld(s + 1u)) + (ld(s + 2u) + ld(s + 3u)));
+    for (; s < k.n_samples; ++s) acc = acc + ld(s);
     if (!k.last) {
         k.acc[3 * i] = acc.x; k.acc[3 * i + 1] = acc.y; k.acc[3 * i + 2] = acc.z;
         return;
@@ -734,7 +707,7 @@ hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid,
 {
     const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;
-    const size_t lds = (variant == V_EXACT_SCALAR) ? 0 : (size_t)p.blob_units * 16u;
+    const size_t lds = (size_t)p.lds_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};
     return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, stream);
 }

@@ -30,8 +30,8 @@ ds = rt.DeviceScene(arrays)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
-# kind:traversal[:kN][:sN] -- traversal "cullN" sets RT_CULL_STRUCTURE=N, "kN" RT_ITEM_BLOCKS=N,
-# "sN" RT_SPLIT_BLOCKS=N
+# kind:traversal[:cN][:LN] -- traversal "cullN" sets RT_CULL_STRUCTURE=N, "cN" RT_CHUNK_ITEMS=N,
+# "L0"/"L1" RT_SHADE_LDS
 variants = [(v.split(":")[0], v.split(":")[1], v.split(":")[2:]) for v in a.variants.split(",")]
 times = {":".join([k, t] + x): [] for k, t, x in variants}
 ref = None
@@ -40,8 +40,8 @@ for r in range(a.rounds + 1):
     for kind, trav, extra in variants:
         if trav.startswith("cull") and len(trav) > 4:
             os.environ["RT_CULL_STRUCTURE"] = trav[4:]
-        os.environ["RT_ITEM_BLOCKS"] = "".join(x[1:] for x in extra if x.startswith("k"))
-        os.environ["RT_SPLIT_BLOCKS"] = "".join(x[1:] for x in extra if x.startswith("s"))
+        os.environ["RT_CHUNK_ITEMS"] = "".join(x[1:] for x in extra if x.startswith("c"))
+        os.environ["RT_SHADE_LDS"] = "".join(x[1:] for x in extra if x.startswith("L"))
         p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
                            brute_force=trav == "brute")
         seg.zero_()

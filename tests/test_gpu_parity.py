@@ -264,27 +264,22 @@ def test_multi_pass_slots_bit_exact(spp, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kblk,split,budget_slots", [(1, 0, 0), (3, 0, 0), (5, 1, 0), (4, 0, 3), (32, 0, 0),
-                                                    (1, 1, 0), (2, 2, 3), (2, 5, 0), (3, 64, 2), (1, 1, 1)])
-def test_item_blocks_bit_exact(kblk, split, budget_slots, monkeypatch):
-    """A work item may cover K consecutive 4-sample blocks of a pixel (RT_ITEM_BLOCKS), and the
-    last blocks of each pass may be traced one sample per item (RT_SPLIT_BLOCKS); each block
-    sum is still formed as ((c0+c1)+(c2+c3)) and lands in its own slot, so any K and split --
-    with ragged last groups, spp % 4 tails and multi-pass slot budgets that cut groups --
-    gives the bits of the oracle."""
+@pytest.mark.parametrize("chunk,budget_samples,shade_lds", [(64, 0, "1"), (128, 0, "0"), (512, 0, ""), (8192, 0, "0"),
+                                                           (64, 4, ""), (512, 8, "1"), (192, 12, "0")])
+def test_chunking_and_passes_bit_exact(chunk, budget_samples, shade_lds, monkeypatch):
+    """Items (one sample of one pixel) are dealt in chunks (RT_CHUNK_ITEMS), a small slot
+    budget (RT_SLOT_BUDGET_BYTES) cuts the samples into passes of a multiple of 4, and the
+    shading records may sit in LDS or global memory (RT_SHADE_LDS); none of it may change the
+    bits: the oracle's frame for spp = 23 (5 blocks of 4 + a 3-sample tail)."""
     s, m = G.scene("huge")
-    W, H, spp = 40, 24, 23  # 5 blocks + 3 tail samples
+    W, H, spp = 40, 24, 23
     p = rt.make_params(W, H, spp, 64, 11)
     cam = O.camera_default(W, H, abi.RT_CAMERA_REFERENCE)
     want, want_seg = O.render_f32(s, m, cam, p)
-    monkeypatch.setenv("RT_ITEM_BLOCKS", "2")
-    monkeypatch.setenv("RT_SPLIT_BLOCKS", "0")
-    base, st0 = rt.render_f32((s, m), p)
-    monkeypatch.setenv("RT_ITEM_BLOCKS", str(kblk))
-    monkeypatch.setenv("RT_SPLIT_BLOCKS", str(split))
-    if budget_slots:
-        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_slots))
-    got, st1 = rt.render_f32((s, m), p)
+    monkeypatch.setenv("RT_CHUNK_ITEMS", str(chunk))
+    monkeypatch.setenv("RT_SHADE_LDS", shade_lds)
+    if budget_samples:
+        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_samples))
+    got, st = rt.render_f32((s, m), p)
     _bits_equal(got, want)
-    _bits_equal(base, want)
-    assert st1.segments == st0.segments == want_seg
+    assert st.segments == want_seg

@@ -21,9 +21,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")
 ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--depth", type=int, default=0, help="override the config's max depth")
 ap.add_argument("--variants", default="exact:cull,exact:brute,fast:cull,fast:brute")
 a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
+depth = a.depth or depth
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H, rt.CORRECTED if a.camera == "corrected" else rt.REFERENCE)
 ds = rt.DeviceScene(arrays)
@@ -77,6 +79,10 @@ for r in range(a.rounds + 1):
                           f"  exit  (frac) {qs([r[1] - t0 for r in tl], T)}\n"
                           f"  iterations   {qs([r[2] for r in tl], 1, 0)}\n"
                           f"  refills      {qs([r[4] for r in tl], 1, 0)}", flush=True)
+                    dump = os.environ.get("RT_TIMELINE_OUT")
+                    if dump:  # raw per-wave records for offline analysis
+                        with open(f"{dump}.{name.replace(':', '_')}.json", "w") as fh:
+                            json.dump(ds.debug_timeline(), fh)
                     late = sorted(tl, key=lambda r: -r[1])[:5]
                     print("  latest waves (start, exit frac, iters, cu, refills):",
                           [(round((r[0] - t0) / T, 3), round((r[1] - t0) / T, 3), r[2], r[3], r[4]) for r in late],

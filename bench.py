@@ -57,7 +57,7 @@ def parse():
                     help="cull: exact cluster culling (same bits); brute: every sphere, as the reference")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=32, help="rows in the CPU-baseline sample")
+    ap.add_argument("--cpu-rows", type=int, default=240, help="rows in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
 

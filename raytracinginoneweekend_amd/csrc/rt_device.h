@@ -51,11 +51,12 @@ struct KParams {
     uint32_t n_pixels, tiles_x, tiled_rows;  // tiled_rows: rows covered by 8x8 tiles (0 = untiled)
     uint32_t sample_begin, sample_end;      // this launch's samples
     uint32_t n_items, n_chunks, chunk_items;  // items dealt per queue grab (multiple of 64)
+    uint32_t n_big_chunks;   // chunks [0, n_big_chunks) hold chunk_items items, the rest 64
     // scene
     uint32_t n_spheres, n_materials;
     // scene blob, staged whole into LDS: [geo: n_geo float4 {cx, cy, cz, fl(r*r)}]
     // [sidx: n_geo u32 original indices, padded to 16 B][clusters: n_clusters x 2 float4].
-    // geo = the always-tested list (n_always, multiple of 8) then each cluster's members
+    // geo = the always-tested list (n_always spheres, padded to 4) then each cluster's members
     // (padded to 8); padding entries have r*r = -inf and never hit.
     const float4 *blob;
     uint32_t blob_units;     // 16-byte units

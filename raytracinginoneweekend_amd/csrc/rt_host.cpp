@@ -79,6 +79,14 @@ uint32_t chunk_items()
     return v >= 64 && v <= 8192 && v % 64 == 0 ? static_cast<uint32_t>(v) : 512u;
 }
 
+// Share of a launch's items dealt in 64-item chunks at its end (RT_TAIL_PCT for A/B, 0-100).
+uint32_t tail_pct()
+{
+    const char *e = std::getenv("RT_TAIL_PCT");
+    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 8ul;
+    return v <= 100 ? static_cast<uint32_t>(v) : 8u;
+}
+
 } // namespace
 
 struct rt_scene {
@@ -99,7 +107,7 @@ struct rt_scene {
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;
     int cu_count = 0;
-    int occ[4][6][2];  // [variant][cull structure][shade records in LDS] blocks per CU, -1 = not queried
+    int occ[4][7][2];  // [variant][cull structure 0-6][shade records in LDS] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
@@ -318,7 +326,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     };
     blob_t b;
     push(always);
-    b.n_always = static_cast<uint32_t>(sidx.size());
+    b.n_always = static_cast<uint32_t>(always.size());  // tested with its exact count (padding after it)
     std::vector<float> crec;
     std::vector<float> boxes;  // per cluster lo/hi (6 floats), for the level-2 boxes
     for (const auto &c : clusters) {
@@ -345,6 +353,12 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
         float pf;
         std::memcpy(&pf, &packed, 4);
         crec.insert(crec.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
+    }
+    // 4 never-hitting entries after the last cluster: structure 6 tests members in blocks of
+    // 8 (a cluster of 4 or 12 reads into its successor, harmless for the (t, index) minimum)
+    for (int i = 0; i < 4; ++i) {
+        geo.insert(geo.end(), {0.f, 0.f, 0.f, -INFINITY});
+        sidx.push_back(0xffffffffu);
     }
     b.n_geo = static_cast<uint32_t>(sidx.size());
     b.n_clusters = static_cast<uint32_t>(clusters.size());
@@ -463,7 +477,8 @@ int cull_structure()
 {
     const char *e = std::getenv("RT_CULL_STRUCTURE");
     const int v = e ? std::atoi(e) : 5;
-    return (v >= 1 && v <= 5) ? v : 5;
+    static_assert(sizeof(rt_scene::occ[0]) / sizeof(rt_scene::occ[0][0]) == 7, "occupancy cache: structures 0-6");
+    return (v >= 1 && v <= 6) ? v : 5;
 }
 
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
@@ -746,7 +761,12 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         k.sample_end = s1;
         fill_frame_consts(k);
         k.n_items = static_cast<uint32_t>(n_pixels * (s1 - s0));
-        k.n_chunks = (k.n_items + k.chunk_items - 1u) / k.chunk_items;
+        {   // the last tail_pct % of the items go out in 64-item chunks (even end-of-launch drain)
+            const uint64_t tail = static_cast<uint64_t>(k.n_items) * tail_pct() / 100u;
+            k.n_big_chunks = static_cast<uint32_t>((k.n_items - tail) / k.chunk_items);
+            const uint32_t rest = k.n_items - k.n_big_chunks * k.chunk_items;
+            k.n_chunks = k.n_big_chunks + (rest + 63u) / 64u;
+        }
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_items + 255u) / 256u)));
         RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), st));

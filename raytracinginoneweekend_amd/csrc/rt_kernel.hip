@@ -180,9 +180,15 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
             dq[k] = b * b - a * c;                                           // :60
         }
     }
-    float m = fmaxf(fmaxf(dq[0], dq[1]), fmaxf(dq[2], dq[3]));
-    if (N == 8) m = fmaxf(m, fmaxf(fmaxf(dq[4 % N], dq[5 % N]), fmaxf(dq[6 % N], dq[7 % N])));
-    if (m > 0.f) {
+    // pairwise max tree (NaN never wins)
+    float mq[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) mq[k] = dq[k];
+#pragma unroll
+    for (int w = N / 2; w >= 1; w /= 2)
+#pragma unroll
+        for (int k = 0; k < w; ++k) mq[k] = fmaxf(mq[k], mq[k + w]);
+    if (mq[0] > 0.f) {
         if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
 #pragma unroll
         for (int k = 0; k < N; ++k) {
@@ -211,7 +217,8 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
 #define RT_PAD_REL 1e-3f
 #define RT_MAX_CLUSTERS 128  // rt_host.cpp sizes clusters so a scene never needs more
 
-// a cluster's members: blocks of 8, then one block of 4 (counts are multiples of 4)
+// a list of spheres: blocks of 8, then 4, then single spheres (cluster member counts are
+// multiples of 4; the always-tested list has its exact count, e.g. 1 for the ground)
 template <bool FAST, bool STATS>
 __device__ __forceinline__ void run_members(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
                                             uint32_t start, uint32_t cnt, f3 o, f3 d, float a, Hit &h, Dbg &dbg)
@@ -219,7 +226,8 @@ __device__ __forceinline__ void run_members(const float4 *__restrict__ geo, cons
     const uint32_t end = start + cnt;
     uint32_t i = start;
     for (; i + 8 <= end; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
-    if (i < end) test_block8<FAST, STATS, 4>(geo, sidx, i, o, d, a, h, dbg);
+    if (i + 4 <= end) { test_block8<FAST, STATS, 4>(geo, sidx, i, o, d, a, h, dbg); i += 4; }
+    for (; i < end; ++i) test_block8<FAST, STATS, 1>(geo, sidx, i, o, d, a, h, dbg);
 }
 
 struct RayBox {  // per-segment constants of the padded slab test
@@ -237,7 +245,7 @@ __device__ __forceinline__ bool box_pass(const RayBox &r, float4 c0, float4 c1, 
 template <bool FAST, int CULL, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
-                                           f3 d, Dbg &dbg, uint32_t &tests)
+                                           f3 d, Dbg &dbg, uint32_t &tests, uint64_t (&cmask)[2])
 {
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
     Hit h{RT_TMAX, 0xffffffffu};
@@ -254,6 +262,28 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float px = pad * aix, py = pad * aiy, pz = pad * aiz;
         const float tb_hi = h.t * 1.002f;
         const float t_lo = 0.5f * RT_TMIN;
+        if (CULL == 6) {
+            // boxes only: the two-level box walk of structure 5 against the always-list t_best,
+            // into a per-lane mask of passing clusters; the members are tested afterwards by
+            // the whole wave on compacted (ray, cluster half) units (members_compacted)
+            const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
+            const float4 *sup = clus + (p.supers_offset - p.clus_offset);
+            for (uint32_t g = 0; g < p.n_supers; ++g) {
+                const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
+                ++tests;
+                if (!box_pass(rb, s0, s1, t_lo, tb_hi)) continue;
+                const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
+                tests += 4;
+                uint32_t bits = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k)
+                    bits |= box_pass(rb, clus[2 * (c0i + k)], clus[2 * (c0i + k) + 1], t_lo, tb_hi) ? (1u << k) : 0u;
+                const uint64_t sh = (uint64_t)bits << (c0i & 63u);
+                if (c0i < 64u) cmask[0] |= sh;
+                else cmask[1] |= sh;
+            }
+            return h;
+        }
         if (CULL == 5) {
             // two levels: a box over each 4 clusters, then pairs of cluster boxes inside
             const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
@@ -367,6 +397,87 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
     return h;
 }
 
+// Structure 6, phase B: the member tests of every (lane, passing cluster) pair of the wave,
+// compacted. A pair is split into two units of 8 member slots (a cluster holds <= 16); the
+// units are numbered by an exclusive prefix over the lanes (bit-plane ballots), dealt 64 per
+// round to ALL lanes of the wave (idle lanes included), and each unit's best candidate is
+// folded into its owner's LDS key with one ds_min_u64: key = bits(t) << 32 | original index,
+// and for t > 0 the u64 order IS the (t, index) lexicographic order of closest_hit, so the
+// result is the same whatever lane tests what, in whatever order. A half-block reading past
+// its cluster tests the next cluster's spheres (or never-hitting padding): extra genuine
+// candidates never change the minimum. Must be called by the whole wave (uniform control).
+template <bool FAST, bool STATS>
+__device__ __forceinline__ void members_compacted(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
+                                                  const float4 *__restrict__ clus, uint64_t *wkey, uint32_t *wlist,
+                                                  const uint64_t (&cmask)[2], f3 o, f3 d, Hit &h, Dbg &dbg,
+                                                  uint32_t &tests)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t k = (uint32_t)(__popcll(cmask[0]) + __popcll(cmask[1]));  // passing clusters
+    // exclusive prefix E of k over the lanes, and the wave total T
+    uint32_t E = 0, T = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+        const uint64_t bb = __ballot((k >> b) & 1u);
+        E += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+        T += (uint32_t)__popcll(bb) << b;
+    }
+    T = __builtin_amdgcn_readfirstlane(T);
+    if (T == 0) return;
+    if (k) wkey[lane] = ((uint64_t)__float_as_uint(h.t) << 32) | h.id;
+    const uint32_t units = 2u * T;
+    for (uint32_t base = 0; base < units; base += 64u) {
+        // emission: each owner writes its units in [base, base + 64)
+        if (k) {
+            uint32_t j = 0;
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                uint64_t m = cmask[w];
+                while (m) {
+                    const uint32_t c = (uint32_t)__builtin_ctzll(m) + 64u * (uint32_t)w;
+                    m &= m - 1u;
+                    const uint32_t u0 = 2u * (E + j++);
+                    if (u0 + 1u >= base && u0 < base + 64u) {
+                        const uint32_t e = lane | (c << 6);
+                        if (u0 >= base) wlist[u0 - base] = e;
+                        if (u0 + 1u < base + 64u) wlist[u0 + 1u - base] = e | (1u << 13);
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t n_here = min(64u, units - base);
+        const uint32_t e = lane < n_here ? wlist[lane] : 0u;
+        const uint32_t owner = e & 63u;
+        // the owner's ray, read across lanes (every lane active here)
+        const f3 ro = mk(__shfl(o.x, owner), __shfl(o.y, owner), __shfl(o.z, owner));
+        const f3 rd = mk(__shfl(d.x, owner), __shfl(d.y, owner), __shfl(d.z, owner));
+        if (lane < n_here) {
+            const uint32_t c = (e >> 6) & 127u, half = e >> 13;
+            const uint32_t sc = __float_as_uint(clus[2 * c + 1].w);
+            const uint32_t start = sc & 0xffffu, cnt = sc >> 16;
+            if (8u * half < cnt) {
+                const float a = rd.x * rd.x + rd.y * rd.y + rd.z * rd.z;
+                Hit u{RT_TMAX, 0xffffffffu};
+                test_block8<FAST, STATS>(geo, sidx, start + 8u * half, ro, rd, a, u, dbg);
+                tests += 8u << 16;
+                if (u.id != 0xffffffffu)
+                    atomicMin((unsigned long long *)(wkey + owner), ((uint64_t)__float_as_uint(u.t) << 32) | u.id);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (k) {
+        const uint64_t key = wkey[lane];
+        h.t = __uint_as_float((uint32_t)(key >> 32));
+        h.id = (uint32_t)key;
+    }
+}
+
 // ---- the megakernel ----------------------------------------------------------------------
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
@@ -399,6 +510,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     const float4 *clus = blob + p.clus_offset;
 
     const uint32_t lane = threadIdx.x & 63u;
+    // structure 6: per-wave LDS scratch of the compacted member tests (owner keys, unit list)
+    uint64_t *wkey = nullptr;
+    uint32_t *wlist = nullptr;
+    if constexpr (CULL == 6) {
+        __shared__ uint64_t s_wkey[4][64];
+        __shared__ uint32_t s_wlist[4][64];
+        wkey = s_wkey[threadIdx.x >> 6];
+        wlist = s_wlist[threadIdx.x >> 6];
+    }
 
     // wave-uniform cursor over the item space
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
@@ -445,8 +565,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     if (++q_tried == 8u) exhausted = true;
                     continue;
                 }
-                cnext = (uint32_t)chunk * p.chunk_items;
-                cend = min(cnext + p.chunk_items, p.n_items);
+                // big chunks first, then 64-item chunks for the end of the launch: a wave
+                // then holds at most 64 undealt items when the queues run dry
+                if (chunk < p.n_big_chunks) {
+                    cnext = (uint32_t)chunk * p.chunk_items;
+                    cend = cnext + p.chunk_items;
+                } else {
+                    cnext = p.n_big_chunks * p.chunk_items + ((uint32_t)chunk - p.n_big_chunks) * 64u;
+                    cend = min(cnext + 64u, p.n_items);
+                }
             }
             const uint32_t avail = cend - cnext;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
@@ -495,19 +622,28 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         if (__ballot(alive) == 0) break;  // only when the item space is exhausted
         if (STATS && lane == 0) ++dbg_iters;
 
-        // ---- one segment for every live lane ------------------------------------------
+        // ---- closest hit of one segment for every live lane -----------------------------
+        const bool seg = alive && depth < p.max_depth;  // depth check: main.cxx:74
+        Hit h{RT_TMAX, 0xffffffffu};
+        uint64_t cmask[2] = {0, 0};
+        uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
+        if (seg) h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, cmask);
+        if constexpr (CULL == 6) members_compacted<FAST, STATS>(geo, sidx, clus, wkey, wlist, cmask, o, d, h, dbg, tally);
+        stamp(2);
+        {
+            const uint32_t al = seg ? p.n_always : 0u;
+            tests_sph += al + (tally >> 16);
+            tests_box += (tally & 0xffffu) - al;
+        }
+
+        // ---- shading: one segment for every live lane ------------------------------------
         if (alive) {
             bool done = false;
             f3 col = mk(0.f, 0.f, 0.f);
-            if (depth >= p.max_depth) {
+            if (!seg) {
                 done = true;  // main.cxx:74 (only reachable with max_depth == 0)
             } else {
                 ++segs;
-                uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
-                const Hit h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally);
-                stamp(2);
-                tests_sph += p.n_always + (tally >> 16);
-                tests_box += (tally & 0xffffu) - p.n_always;
                 const float t = h.t;
                 const uint32_t ib = h.id;
                 ++depth;
@@ -689,6 +825,7 @@ template <int V, bool STATS> static const void *ptr3(int cull)
     if (cull == 3) return reinterpret_cast<const void *>(&render_kernel<V, 3, STATS>);
     if (cull == 4) return reinterpret_cast<const void *>(&render_kernel<V, 4, STATS>);
     if (cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS>);
+    if (cull == 6) return reinterpret_cast<const void *>(&render_kernel<V, 6, STATS>);
     return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS>);
 }
 

@@ -189,7 +189,7 @@ def _random_scene(rng, n, spread, center=(0.0, 0.0, 0.0)):
     (3, 400, 3.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
     (4, 800, 5.0, (200.0, 0.0, -150.0), abi.RT_CAMERA_CORRECTED),
 ])
-@pytest.mark.parametrize("structure", ["1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("structure", ["1", "2", "3", "4", "5", "6"])
 def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, structure, monkeypatch):
     monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
     rng = np.random.default_rng(seed)

@@ -105,7 +105,7 @@ struct rt_scene {
     size_t slots_bytes = 0;
     float *acc = nullptr;
     size_t acc_bytes = 0;
-    uint32_t *queue_ctr = nullptr;
+    uint32_t *queue_ctr = nullptr;  // 8 queue counters, one 256-B line each
     int cu_count = 0;
     int occ[4][7][2];  // [variant][cull structure 0-6][shade records in LDS] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
@@ -409,6 +409,29 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
         b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
         ++b.n_supers;
     }
+    // level 3: one box over every cluster (after the level-2 boxes)
+    {
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t c = 0; c < b.n_clusters_real; ++c)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], boxes[6 * c + a]);
+                hi[a] = std::max(hi[a], boxes[6 * c + 3 + a]);
+            }
+        float C[3] = {0.f, 0.f, 0.f}, E[3] = {-1e30f, -1e30f, -1e30f};
+        float kc = 0.f;
+        if (lo[0] <= hi[0]) {
+            for (int a = 0; a < 3; ++a) {
+                C[a] = .5f * (lo[a] + hi[a]);
+                E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
+            }
+            kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
+            b.clus_pad = std::max(b.clus_pad, kc);
+        }
+        uint32_t packed = 0;
+        float pf;
+        std::memcpy(&pf, &packed, 4);
+        b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
+    }
     return b;
 }
 
@@ -481,6 +504,15 @@ int cull_structure()
     return (v >= 1 && v <= 6) ? v : 5;
 }
 
+// RT_ROOT_BOX=0 disables the level-3 box gate (A/B); same bits either way.
+uint32_t root_box_env()
+{
+    const char *e = std::getenv("RT_ROOT_BOX");
+    return e && e[0] == '0' ? 0u : 1u;
+}
+
+
+
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
 bool debug_stats()
 {
@@ -544,7 +576,8 @@ int rt_scene_destroy(rt_scene *sc)
     (void)hipSetDevice(sc->device);
     for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
     for (auto e : sc->ev_end) (void)hipEventDestroy(e);
-    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc, (void *)sc->queue_ctr})
+    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc,
+                    (void *)sc->queue_ctr})
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
     delete sc;
@@ -714,6 +747,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.n_clusters_real = sc->n_clusters_real[b];
     k.n_supers = sc->n_supers[b];
     k.supers_offset = sc->supers_offset[b];
+    k.use_root = root_box_env();
     k.shade_offset = sc->shade_offset[b];
     // the shading records (the blob's tail) join the geometry in LDS unless that costs
     // workgroups per CU; RT_SHADE_LDS=0/1 forces the choice for A/B
@@ -754,6 +788,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
 
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
+    RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     for (uint32_t s0 = 0; s0 < P.spp; s0 += static_cast<uint32_t>(spp_pass)) {
         const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
@@ -770,7 +805,6 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_items + 255u) / 256u)));
         RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), st));
-        if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
         if (verbose())
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) chunk=%u\n",
                          variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1, k.chunk_items);

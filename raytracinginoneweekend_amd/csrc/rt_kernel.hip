@@ -188,6 +188,7 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
     for (int w = N / 2; w >= 1; w /= 2)
 #pragma unroll
         for (int k = 0; k < w; ++k) mq[k] = fmaxf(mq[k], mq[k + w]);
+#ifdef RT_DIVERGENT_ROOTS  // A/B build: lane-divergent branches around the root work
     if (mq[0] > 0.f) {
         if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
 #pragma unroll
@@ -205,6 +206,33 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
             }
         }
     }
+#else
+    // Wave-uniform branches (ballots) around the root work, lane selects inside: a masked
+    // lane costs the same issue slots as a computing one, and uniform branches need no
+    // exec-mask save/restore. Lanes without a positive discriminant compute throw-away
+    // values (sqrt of a negative is NaN) and are excluded by `pos` in the final select.
+    if (__ballot(mq[0] > 0.f)) {
+        if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const bool pos = dq[k] > 0.f;                                    // :62
+            if (__ballot(pos)) {
+                if (STATS) { dbg.lane_roots += pos; if (first_active_lane()) ++dbg.wave_roots; }
+                const float q = sqrtf(dq[k]);
+                float t = (-bq[k] - q) / a;                                  // :63
+                const bool ok = t < RT_TMAX && t > RT_TMIN;
+                if (__ballot(pos && !ok)) {
+                    const float t2 = (-bq[k] + q) / a;                       // :76
+                    t = ok ? t : (t2 < RT_TMAX && t2 > RT_TMIN ? t2 : __builtin_nanf(""));
+                } else {
+                    t = ok ? t : __builtin_nanf("");
+                }
+                const uint32_t id = sidx[i + k];
+                if (pos && (t < h.t || (t == h.t && id < h.id))) { h.t = t; h.id = id; }
+            }
+        }
+    }
+#endif
 }
 
 // Cluster culling: a lane tests a cluster's spheres only if its ray segment (kMIN, t_best]
@@ -242,6 +270,18 @@ __device__ __forceinline__ bool box_pass(const RayBox &r, float4 c0, float4 c1, 
     return tin <= tout && tout >= t_lo && tin <= t_hi;
 }
 
+// Level 3: one box over every cluster (stored after the level-2 boxes). When no lane's
+// segment reaches it, the wave skips the level-2 loop (returns 0 supers to walk): a ray
+// that misses the padded union box misses every padded box inside it.
+__device__ __forceinline__ uint32_t root_gate(const KParams &p, const RayBox &rb, const float4 *sup, float t_lo,
+                                              float t_hi, uint32_t &tests)
+{
+    if (!p.use_root) return p.n_supers;
+    ++tests;
+    const bool pass = box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, t_hi);
+    return __ballot(pass) ? p.n_supers : 0u;
+}
+
 template <bool FAST, int CULL, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
@@ -268,7 +308,8 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
             // the whole wave on compacted (ray, cluster half) units (members_compacted)
             const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
             const float4 *sup = clus + (p.supers_offset - p.clus_offset);
-            for (uint32_t g = 0; g < p.n_supers; ++g) {
+            const uint32_t n_supers = root_gate(p, rb, sup, t_lo, tb_hi, tests);
+            for (uint32_t g = 0; g < n_supers; ++g) {
                 const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
                 ++tests;
                 if (!box_pass(rb, s0, s1, t_lo, tb_hi)) continue;
@@ -288,7 +329,8 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
             // two levels: a box over each 4 clusters, then pairs of cluster boxes inside
             const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
             const float4 *sup = clus + (p.supers_offset - p.clus_offset);
-            for (uint32_t g = 0; g < p.n_supers; ++g) {
+            const uint32_t n_supers = root_gate(p, rb, sup, t_lo, tb_hi, tests);
+            for (uint32_t g = 0; g < n_supers; ++g) {
                 const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
                 ++tests;
                 if (!box_pass(rb, s0, s1, t_lo, h.t * 1.002f)) continue;
@@ -531,9 +573,14 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     f3 o = mk(0.f, 0.f, 0.f), d = o, att = o;
     uint32_t depth = 0;
     uint64_t rng = 0;
+    // a lambert/metal hit leaves its scatter offset to the next iteration's rejection loop:
+    // o = hit point; d = p + n (lambert) or reflect(unit(d), n) (metal); pn = n, roughness
+    bool pend = false, pend_metal = false;
+    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t segs = 0, tests_sph = 0, tests_box = 0;  // per-lane tallies (widened at the end)
     Dbg dbg{0, 0, 0, 0, 0};
-    uint32_t dbg_iters = 0, dbg_refills = 0;
+    uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0;
+    uint64_t t_dry = 0;  // STATS: realtime when this wave found every queue empty
     // STATS build only: shader-clock cycles per loop region, summed over the wave's iterations
     uint64_t cyc[5] = {0, 0, 0, 0, 0};  // refill, sample start, closest hit, shading, fold
     uint64_t t_prev = STATS ? __builtin_amdgcn_s_memtime() : 0;
@@ -590,37 +637,74 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         }
 
         stamp(0);
-        // ---- start the sample of a freshly assigned item -----------------------------
+        // ---- start the sample of a freshly assigned item (main.cxx:192-200) -----------
+        const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
+        uint64_t rc = 0;  // the camera stream of a fresh sample
+        float uu = 0.f, vv = 0.f;
         if (fresh) {
             uint32_t px, rr;
             pixel_of(*fc, pix, px, rr);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
             const uint32_t s = fc->sample_begin + ls;
             const uint64_t key = ((uint64_t)py * fc->W + px) * fc->spp + s;
-            const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
             const uint64_t inc_cam = ((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo;
             rng = pcg_seed(key, inc_data);
-            uint64_t rc = pcg_seed(key, inc_cam);
-            // main.cxx:192-200
+            rc = pcg_seed(key, inc_cam);
             const float fW = fc->fW, fH = fc->fH;
             const float u = (float)px / fW;
             const float v = (float)py / fH;
-            const float uu = u + canonical(rng, inc_data) / fW;
-            const float vv = v + canonical(rng, inc_data) / fH;
-            // camera.hxx:46-57
-            const f3 rd = random_in_unit_sphere(rc, inc_cam) * fc->lens;
-            const f3 off = mk(uu * rd.x, vv * rd.y, 0.f);
-            const f3 org = mk(fc->org[0], fc->org[1], fc->org[2]);
-            o = org + off;
-            d = ((mk(fc->llc[0], fc->llc[1], fc->llc[2]) + mk(fc->hor[0], fc->hor[1], fc->hor[2]) * uu) +
-                 mk(fc->ver[0], fc->ver[1], fc->ver[2]) * (1.f - vv)) - off;
-            if (fc->corrected) d = d - org;
+            uu = u + canonical(rng, inc_data) / fW;
+            vv = v + canonical(rng, inc_data) / fH;
             att = mk(1.f, 1.f, 1.f);
             depth = 0;
         }
+        // ---- one rejection loop for the wave (raytracer.hxx:32-43) ------------------------
+        // Fresh lanes draw the lens offset from their camera stream (camera.hxx:52); lanes
+        // whose last hit was lambert or metal draw their scatter offset from their data stream
+        // (raytracer.hxx:135,147). Serving both in ONE loop makes the wave pay the longest
+        // rejection run of the union of those lanes once per iteration instead of once per
+        // kind; every stream still sees exactly its own draws in its own order.
+        if (fresh || pend) {
+            const uint64_t inc = fresh ? (((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo) : inc_data;
+            uint64_t st = fresh ? rc : rng;
+            const f3 r = random_in_unit_sphere(st, inc);
+            if (fresh) {
+                // camera.hxx:46-57
+                const f3 rd = r * fc->lens;
+                const f3 off = mk(uu * rd.x, vv * rd.y, 0.f);
+                const f3 org = mk(fc->org[0], fc->org[1], fc->org[2]);
+                o = org + off;
+                d = ((mk(fc->llc[0], fc->llc[1], fc->llc[2]) + mk(fc->hor[0], fc->hor[1], fc->hor[2]) * uu) +
+                     mk(fc->ver[0], fc->ver[1], fc->ver[2]) * (1.f - vv)) - off;
+                if (fc->corrected) d = d - org;
+            } else {
+                rng = st;
+                if (!pend_metal) {
+                    d = (d + r) - o;                       // lambert :135, d held p + n, o = p
+                } else {
+                    const f3 nd = d + r * pn.w;            // metal :147, d held reflect(unit(d), n)
+                    if (dot(nd, mk(pn.x, pn.y, pn.z)) > 0.f) {
+                        d = nd;
+                    } else {                               // absorbed: main.cxx:68, colour 0
+                        alive = false;
+                        float *dst = p.slots + ((size_t)ls * fc->n_pixels + pix) * 3u;
+                        dst[0] = 0.f;
+                        dst[1] = 0.f;
+                        dst[2] = 0.f;
+                    }
+                }
+                pend = false;
+            }
+        }
         stamp(1);
         if (__ballot(alive) == 0) break;  // only when the item space is exhausted
-        if (STATS && lane == 0) ++dbg_iters;
+        if (STATS && lane == 0) {
+            ++dbg_iters;
+            if (exhausted) {
+                if (!dbg_iters_dry) t_dry = __builtin_amdgcn_s_memrealtime();
+                ++dbg_iters_dry;
+            }
+        }
 
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && depth < p.max_depth;  // depth check: main.cxx:74
@@ -636,7 +720,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             tests_box += (tally & 0xffffu) - al;
         }
 
-        // ---- shading: one segment for every live lane ------------------------------------
+        // ---- shading: the hit of every live lane -----------------------------------------
         if (alive) {
             bool done = false;
             f3 col = mk(0.f, 0.f, 0.f);
@@ -652,6 +736,10 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     const float tt = .5f * normalize(d).y + 1.f;
                     const f3 bg = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
                     col = bg * att;
+                    done = true;
+                } else if (depth >= p.max_depth) {
+                    // main.cxx:65-74: a scattered ray would not be traced and an absorbed one
+                    // returns 0 too; this sample's streams are not drawn from again
                     done = true;
                 } else {
                     float4 sf, md;
@@ -670,23 +758,22 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                     const f3 ctr = mk(sf.x, sf.y, sf.z);
                     const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
                     const f3 hn = (hp - ctr) / sf.w;            // raytracer.hxx:71
-                    const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
-                    const f3 albedo = mk(md.x, md.y, md.z);
-                    bool scattered = true;
-                    f3 nd;
-                    // raytracer.hxx:120-199. Lambert and metal lanes share one rejection loop and
-                    // metal and dielectric lanes one normalize (the draw order is unchanged:
-                    // reflect() consumes no draws).
-                    f3 ud = d;
-                    if (kind != 0u) ud = normalize(d);
-                    f3 r = mk(0.f, 0.f, 0.f);
-                    if (kind != 2u) r = random_in_unit_sphere(rng, inc_data);
+                    att = att * mk(md.x, md.y, md.z);           // main.cxx:65 (unused if absorbed)
+                    // raytracer.hxx:120-199
                     if (kind == 0u) {                           // lambert, :132-141
-                        nd = ((hp + hn) + r) - hp;
+                        o = hp;
+                        d = hp + hn;                            // + rius next iteration, then - p
+                        pend = true;
+                        pend_metal = false;
                     } else if (kind == 1u) {                    // metal, :143-156
-                        nd = reflect(ud, hn) + r * md.w;
-                        scattered = dot(nd, hn) > 0.f;
+                        const f3 ud = normalize(d);
+                        o = hp;
+                        d = reflect(ud, hn);                    // + rius * roughness next iteration
+                        pn = make_float4(hn.x, hn.y, hn.z, md.w);
+                        pend = true;
+                        pend_metal = true;
                     } else {                                    // dielectric, :158-194
+                        const f3 ud = normalize(d);
                         f3 outward = mk(-hn.x, -hn.y, -hn.z);
                         float ri = md.w;
                         float cosv = dot(ud, hn);
@@ -699,15 +786,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                         float prob = 1.f;
                         // length(refr) > 0 <=> norm > 0 (correctly rounded sqrt; NaN -> false)
                         if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick(ri, cosv);
-                        nd = canonical(rng, inc_data) < prob ? reflect(ud, hn) : refr;
-                    }
-                    if (!scattered) {
-                        done = true;                            // main.cxx:68
-                    } else {
                         o = hp;
-                        d = nd;
-                        att = att * albedo;                     // main.cxx:65
-                        if (depth >= p.max_depth) done = true;  // main.cxx:74
+                        d = canonical(rng, inc_data) < prob ? reflect(ud, hn) : refr;
                     }
                 }
             }
@@ -744,16 +824,20 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
             if (lane == 0) atomicAdd(p.dbg + i, v);
         }
-        if (lane == 0)
+        if (lane == 0) {
             for (int i = 0; i < 5; ++i) atomicAdd(p.dbg + 8 + i, (unsigned long long)cyc[i]);
-        // wave timeline: [16 + 4w] start, [17 + 4w] exit (realtime ticks), [18 + 4w] loop iterations,
-        // [19 + 4w] hardware id << 32 | refill rounds; w = wave of the grid
+            atomicMax(p.dbg + 14, ~t_wave0);  // launch start = ~max(~t) = earliest wave start
+        }
+        // wave timeline: [16 + 4w] time the queues were found dry (realtime ticks), [17 + 4w] exit,
+        // [18 + 4w] loop iterations, [19 + 4w] hardware id << 32 | iterations after dry << 16 |
+        // refill rounds; w = wave of the grid. The launch starts at t_wave0 of the earliest wave.
         const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (lane == 0 && w < kDbgWaves) {
-            p.dbg[16 + 4 * w] = t_wave0;
+            p.dbg[16 + 4 * w] = t_dry ? t_dry : __builtin_amdgcn_s_memrealtime();
             p.dbg[17 + 4 * w] = __builtin_amdgcn_s_memrealtime();
             p.dbg[18 + 4 * w] = dbg_iters;
-            p.dbg[19 + 4 * w] = ((unsigned long long)__smid() << 32) | dbg_refills;
+            p.dbg[19 + 4 * w] = ((unsigned long long)__smid() << 32) | (min(dbg_iters_dry, 65535u) << 16) |
+                                min(dbg_refills, 65535u);
         }
     }
 }

@@ -104,16 +104,19 @@ class DeviceScene:
         check(lib().rt_scene_debug_counters(self.handle, buf, 1 if reset else 0))
         keys = ["wave_iters", "wave_refills", "wave_blocks", "lane_blocks", "wave_roots", "lane_roots", "segments",
                 "wave_member_blocks", "cyc_refill", "cyc_start", "cyc_hit", "cyc_shade", "cyc_fold"]
-        return dict(zip(keys, list(buf)))
+        out = dict(zip(keys, list(buf)))
+        out["launch_start"] = (~buf[14]) & 0xffffffffffffffff if buf[14] else 0  # 100 MHz ticks
+        return out
 
     def debug_timeline(self, max_waves=65536):
-        """Per-wave (start, exit, iterations, cu_id, refills) of the last instrumented launch
-        (RT_DEBUG_STATS=1; times in ticks of the 100 MHz clock), see rt_scene_debug_timeline."""
+        """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry) of the last
+        instrumented launch (RT_DEBUG_STATS=1; dry = when the wave found every queue empty; times
+        in ticks of the 100 MHz clock), see rt_scene_debug_timeline."""
         buf = (C.c_uint64 * (4 * max_waves))()
         n = C.c_uint32(0)
         check(lib().rt_scene_debug_timeline(self.handle, buf, max_waves, C.byref(n)))
-        return [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], buf[4 * i + 3] >> 32, buf[4 * i + 3] & 0xffffffff)
-                for i in range(n.value)]
+        return [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], buf[4 * i + 3] >> 32, buf[4 * i + 3] & 0xffff,
+                 (buf[4 * i + 3] >> 16) & 0xffff) for i in range(n.value)]
 
     def close(self):
         if self.handle:

@@ -33,7 +33,7 @@ out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
 # kind:traversal[:cN][:LN][:tN] -- traversal "cullN" sets RT_CULL_STRUCTURE=N, "cN" RT_CHUNK_ITEMS=N,
-# "L0"/"L1" RT_SHADE_LDS, "tN" RT_TAIL_PCT=N
+# "L0"/"L1" RT_SHADE_LDS, "tN" RT_TAIL_PCT=N, "r0"/"r1" RT_ROOT_BOX, "s0" no counters
 variants = [(v.split(":")[0], v.split(":")[1], v.split(":")[2:]) for v in a.variants.split(",")]
 times = {":".join([k, t] + x): [] for k, t, x in variants}
 ref = None
@@ -45,10 +45,12 @@ for r in range(a.rounds + 1):
         os.environ["RT_CHUNK_ITEMS"] = "".join(x[1:] for x in extra if x.startswith("c"))
         os.environ["RT_SHADE_LDS"] = "".join(x[1:] for x in extra if x.startswith("L"))
         os.environ["RT_TAIL_PCT"] = "".join(x[1:] for x in extra if x.startswith("t"))
+        os.environ["RT_ROOT_BOX"] = "".join(x[1:] for x in extra if x.startswith("r"))
         p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
                            brute_force=trav == "brute")
         seg.zero_()
-        ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr())
+        count = not any(x == "s0" for x in extra)  # "s0": no segment counters (no end-of-kernel atomics)
+        ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr() if count else None)
         torch.cuda.synchronize()
         ms = ds.kernel_times(1)[0]
         name = ":".join([kind, trav] + extra)
@@ -64,29 +66,32 @@ for r in range(a.rounds + 1):
                   f"mean|d|={d.mean().item():.3g} px<=1e-4: {(px <= 1e-4).float().mean().item()*100:.3f}% "
                   f"px<=1e-3: {(px <= 1e-3).float().mean().item()*100:.3f}%", flush=True)
             if os.environ.get("RT_DEBUG_STATS") == "1":
-                print(f"{name}: counters {ds.debug_counters()}", flush=True)
-                tl = [r for r in ds.debug_timeline() if r[1] > r[0]]
+                cnt = ds.debug_counters()
+                print(f"{name}: counters {cnt}", flush=True)
+                tl = [r for r in ds.debug_timeline() if r[1] >= r[0] > 0]
                 if tl:  # wave concurrency over the launch: how much of it is drain
-                    t0 = min(r[0] for r in tl)
+                    t0 = cnt["launch_start"] or min(r[0] for r in tl)
                     T = max(r[1] for r in tl) - t0
 
                     def qs(vals, scale=1.0, nd=3):
                         v = sorted(vals)
                         return {f"p{int(f * 100)}": round(v[min(len(v) - 1, int(f * len(v)))] / scale, nd)
                                 for f in (0.0, 0.01, 0.1, 0.5, 0.9, 0.99, 1.0)}
-                    busy = sum(r[1] - r[0] for r in tl) / (len(tl) * T)
+                    busy = sum(r[1] - t0 for r in tl) / (len(tl) * T)
                     print(f"{name}: waves={len(tl)} launch={T / 1e5:.3f}ms mean wave occupancy {busy:.3f}\n"
-                          f"  start (frac) {qs([r[0] - t0 for r in tl], T)}\n"
+                          f"  dry   (frac) {qs([r[0] - t0 for r in tl], T)}\n"
                           f"  exit  (frac) {qs([r[1] - t0 for r in tl], T)}\n"
+                          f"  drain (frac) {qs([r[1] - r[0] for r in tl], T)}\n"
                           f"  iterations   {qs([r[2] for r in tl], 1, 0)}\n"
+                          f"  iters after dry {qs([r[5] for r in tl], 1, 0)}\n"
                           f"  refills      {qs([r[4] for r in tl], 1, 0)}", flush=True)
                     dump = os.environ.get("RT_TIMELINE_OUT")
                     if dump:  # raw per-wave records for offline analysis
                         with open(f"{dump}.{name.replace(':', '_')}.json", "w") as fh:
                             json.dump(ds.debug_timeline(), fh)
                     late = sorted(tl, key=lambda r: -r[1])[:5]
-                    print("  latest waves (start, exit frac, iters, cu, refills):",
-                          [(round((r[0] - t0) / T, 3), round((r[1] - t0) / T, 3), r[2], r[3], r[4]) for r in late],
+                    print("  latest waves (dry, exit frac, iters, cu, refills, iters after dry):",
+                          [(round((r[0] - t0) / T, 3), round((r[1] - t0) / T, 3), r[2], r[3], r[4], r[5]) for r in late],
                           flush=True)
         else:
             times[name].append(ms)
@@ -96,6 +101,6 @@ for name, t in times.items():
     res[name] = {"median_ms": round(statistics.median(t), 3), "min_ms": round(min(t), 3),
                  "mrays": round(prim / statistics.median(t) / 1e3, 1),
                  "exec_tflops": round((segs[name][1] * 20 + segs[name][2] * 19) / statistics.median(t) / 1e9, 2),
-                 "tests_per_seg": round(segs[name][1] / segs[name][0], 1),
-                 "boxes_per_seg": round(segs[name][2] / segs[name][0], 1)}
+                 "tests_per_seg": round(segs[name][1] / max(1, segs[name][0]), 1),
+                 "boxes_per_seg": round(segs[name][2] / max(1, segs[name][0]), 1)}
     print(name, json.dumps(res[name]), flush=True)

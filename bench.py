@@ -7,6 +7,11 @@ the HIP megakernel into HBM, the per-rank tiles are gathered to rank 0 over RCCL
 de-interleaved into the frame. Inputs (scene, camera) are resident in HBM before timing.
 value = W*H*spp primary rays per frame * steps / max-over-ranks time (whole job).
 
+Consecutive frames are in flight together (rt_render_device runs each render kernel on an
+internal stream with a double-buffered workspace; results still land in caller-stream order),
+so ms_per_step is the steady-state frame time; frame_latency_ms is one frame alone, start to
+finish (render + accumulate + gather), timed synchronously after the timed loop.
+
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
@@ -59,7 +64,22 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=240, help="rows in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_render_c3.json"),
+                    help="PMC summary of this kernel (scripts/pmc_round.sh) for roofline.traffic / VALU busy")
     return ap.parse_args()
+
+
+def pmc_fields(path, kernel, config):
+    """HBM traffic and VALU issue of the render kernel from a committed rocprofv3 --pmc summary
+    (scripts/pmc_json.py) of the same kernel and workload; None when absent or mismatched."""
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if rec.get("kernel") != kernel or rec.get("config") != config:
+        return None
+    return rec
 
 
 def cpu_baseline(cfg, camera, seed, rows, threads):
@@ -148,6 +168,21 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kt = ds.kernel_times(args.steps)  # render-kernel durations of the timed steps (HIP events)
+    # one frame alone (no frame in flight beside it): its latency, median of 3
+    lat = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        t1 = time.perf_counter()
+        step(False)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t1)
+    latency = sorted(lat)[1]
+    if distributed:
+        t = torch.tensor([latency], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        latency = float(t.item())
     segments, sph_tests, box_tests = [int(x) for x in seg.tolist()]
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -187,6 +222,8 @@ def main():
                        "kernel": ("fast (FMA, stated tolerance)" if args.variant == "fast" else f"{args.variant} (bit-exact)")
                        + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
             "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
+            "frame_latency_ms": round(latency * 1e3, 3),
+            "frames_in_flight": 1 if os.environ.get("RT_PIPELINE") == "0" else 2,
             "segments_per_primary": round(segments_all / primaries, 4),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
@@ -194,8 +231,21 @@ def main():
                          "flop_per_launch": flop_per_launch, "work": "executed sphere+box tests",
                          "brute_force_equiv_tflops": round(brute_equiv, 2)},
             "tests_per_segment": round(sph_tests / max(segments, 1), 2),
+            "kernel_tests_per_s": round(sph_tests / args.steps / (k_avg_ms * 1e-3) / 1e12, 4),
             "boxes_per_segment": round(box_tests / max(segments, 1), 2),
         }
+        v = {"exact": 0, "scalar": 1, "fast": 2}[args.variant]
+        cull = 0 if args.traversal == "brute" or v == 1 else int(os.environ.get("RT_CULL_STRUCTURE", "5"))
+        kname = f"render_kernel<{v}, {cull}, false>"
+        pmc = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
+                                            "traversal": args.traversal, "n_gpus": world})
+        if pmc:
+            # HBM bytes per launch (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE) and
+            # the VALU issue fraction, from the committed PMC summary of this kernel
+            rec["roofline"]["traffic"] = pmc["hbm_bytes_per_launch"]
+            rec["roofline"]["traffic_unit"] = "bytes/launch"
+            rec["roofline"]["valu_busy"] = pmc["valu_busy"]
+            rec["roofline"]["pmc_source"] = os.path.relpath(args.pmc, REPO)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], args.camera, args.seed, args.cpu_rows,
                                                args.cpu_threads)

@@ -86,6 +86,9 @@ struct KAccum {
     uint32_t n_blocks;       // full blocks of 4 among this pass's samples (the rest is the tail)
     uint32_t first, last, spp;
     uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame;
+    // frames in flight: thread 0 adds the render's internal segment counters to the caller's
+    const unsigned long long *seg_from;
+    unsigned long long *seg_to;
 };
 
 // queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise

@@ -61,6 +61,7 @@ hv hnorm(hv a)
 hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x}; }
 
 constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 GiB)
+constexpr size_t kCtrWords = 16 * rt::kQueueStride + 16;  // 2 x 8 queue lines + 2 x 4 u64 segment counters
 
 // RT_SLOT_BUDGET_BYTES lowers the per-pass slot workspace (tests force multi-pass renders).
 uint64_t slot_budget()
@@ -100,12 +101,16 @@ struct rt_scene {
     float clus_pad[2] = {0.f, 0.f};
     uint32_t n_clusters_real[2] = {0, 0}, n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     uint32_t shade_offset[2] = {0, 0};
-    // workspace
-    float *slots = nullptr;
-    size_t slots_bytes = 0;
+    // workspace, double-buffered for two frames in flight: render i runs on internal stream
+    // xs[i % 2] into slots[i % 2] while the caller stream still accumulates frame i - 1
+    float *slots[2] = {nullptr, nullptr};
+    size_t slots_bytes[2] = {0, 0};
     float *acc = nullptr;
     size_t acc_bytes = 0;
-    uint32_t *queue_ctr = nullptr;  // 8 queue counters, one 256-B line each
+    uint32_t *queue_ctr = nullptr;  // [2][8 queues x kQueueStride], then [2][3] u64 segment counters
+    hipStream_t xs[2] = {nullptr, nullptr};
+    hipEvent_t ev_done[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+    bool free_valid[2] = {false, false};  // 8 queue counters, one 256-B line each
     int cu_count = 0;
     int occ[4][7][2];  // [variant][cull structure 0-6][shade records in LDS] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
@@ -513,6 +518,13 @@ uint32_t root_box_env()
 
 
 
+// RT_PIPELINE=0 runs the render kernels on the caller stream (no frames in flight).
+bool pipeline_env()
+{
+    const char *e = std::getenv("RT_PIPELINE");
+    return !(e && e[0] == '0');
+}
+
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
 bool debug_stats()
 {
@@ -576,8 +588,14 @@ int rt_scene_destroy(rt_scene *sc)
     (void)hipSetDevice(sc->device);
     for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
     for (auto e : sc->ev_end) (void)hipEventDestroy(e);
-    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->slots, (void *)sc->acc,
-                    (void *)sc->queue_ctr})
+    for (int b = 0; b < 2; ++b) {
+        if (sc->xs[b]) (void)hipStreamSynchronize(sc->xs[b]);
+        if (sc->xs[b]) (void)hipStreamDestroy(sc->xs[b]);
+        if (sc->ev_done[b]) (void)hipEventDestroy(sc->ev_done[b]);
+        if (sc->ev_free[b]) (void)hipEventDestroy(sc->ev_free[b]);
+    }
+    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->slots[0],
+                    (void *)sc->slots[1], (void *)sc->acc, (void *)sc->queue_ctr})
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
     delete sc;
@@ -648,8 +666,14 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         sc->shade_offset[b] = blobs[b].shade_offset;
     }
     if (rc == RT_OK) {
-        hipError_t e = hipMalloc((void **)&sc->queue_ctr, 8 * rt::kQueueStride * sizeof(uint32_t));
+        hipError_t e = hipMalloc((void **)&sc->queue_ctr, kCtrWords * sizeof(uint32_t));
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+        for (int b = 0; b < 2 && rc == RT_OK; ++b) {
+            if (hipStreamCreateWithFlags(&sc->xs[b], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&sc->ev_done[b], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&sc->ev_free[b], hipEventDisableTiming) != hipSuccess)
+                rc = fail(RT_ERR_DEVICE, "rt_scene_create: stream/event creation failed");
+        }
     }
     if (rc == RT_OK) {
         hipDeviceProp_t prop;
@@ -715,8 +739,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.tiled_rows = tiled ? (k.num_rows / 8u) * 8u : 0u;
     k.n_spheres = sc->n_spheres;
     k.n_materials = sc->n_materials;
-    k.queue_ctr = sc->queue_ctr;
-    k.segments = reinterpret_cast<unsigned long long *>(d_segments);
+
 
     // Variant: exact (bit-exact) or fast (tolerance); clustered culling unless brute force is
     // asked for; the scalar-cache A/B variant is brute force only. Each needs its blob in LDS.
@@ -780,15 +803,28 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     if (spp_pass == 0) spp_pass = 4;
     if (n_pixels * std::min<uint64_t>(spp_pass, P.spp) >= (1ull << 31) - 8192)
         return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
-    if (int rc = ensure((void **)&sc->slots, &sc->slots_bytes, per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc) return rc;
+    // frames in flight: the render kernels of this call run on internal stream xs[b] with
+    // workspace b, ordered only after the caller-stream work that last read workspace b (the
+    // accumulation of call i - 2); they touch no caller memory, so the caller stream sees the
+    // same results in the same order. RT_PIPELINE=0: everything on the caller stream.
+    const uint32_t wb = static_cast<uint32_t>(sc->calls & 1u);
+    const bool pipe = pipeline_env();
+    hipStream_t xst = pipe ? sc->xs[wb] : st;
+    if (int rc = ensure((void **)&sc->slots[wb], &sc->slots_bytes[wb], per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc)
+        return rc;
     if (spp_pass < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
-    k.slots = sc->slots;
+    k.slots = sc->slots[wb];
     k.chunk_items = chunk_items();
+    k.queue_ctr = sc->queue_ctr + wb * 8u * rt::kQueueStride;
+    unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + 16u * rt::kQueueStride) + 4u * wb;
+    k.segments = d_segments ? (pipe ? seg_b : reinterpret_cast<unsigned long long *>(d_segments)) : nullptr;
+    if (pipe && sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(xst, sc->ev_free[wb], 0));
+    if (pipe && d_segments) RT_HIP(hipMemsetAsync(seg_b, 0, 3 * sizeof(unsigned long long), xst));
 
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
-    RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
+    RT_HIP(hipEventRecord(sc->ev_begin[ring], xst));
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     for (uint32_t s0 = 0; s0 < P.spp; s0 += static_cast<uint32_t>(spp_pass)) {
         const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
@@ -804,15 +840,20 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         }
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_items + 255u) / 256u)));
-        RT_HIP(hipMemsetAsync(sc->queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), st));
+        if (pipe && s0 > 0) RT_HIP(hipStreamWaitEvent(xst, sc->ev_free[wb], 0));  // previous pass accumulated
+        RT_HIP(hipMemsetAsync(k.queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), xst));
         if (verbose())
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) chunk=%u\n",
                          variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1, k.chunk_items);
-        RT_HIP(rt::launch_render(variant, cull_mode, k, grid, st));
+        RT_HIP(rt::launch_render(variant, cull_mode, k, grid, xst));
         if (variant == rt::V_STATS_LDS) sc->dbg_waves = grid * 4u;
-        if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], st));
+        if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], xst));
+        if (pipe) {
+            RT_HIP(hipEventRecord(sc->ev_done[wb], xst));
+            RT_HIP(hipStreamWaitEvent(st, sc->ev_done[wb], 0));
+        }
         rt::KAccum a{};
-        a.slots = sc->slots;
+        a.slots = sc->slots[wb];
         a.acc = sc->acc;
         a.out = d_rgb;
         a.out_u8 = nullptr;
@@ -828,7 +869,12 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         a.row_offset = k.row_offset;
         a.row_stride = k.row_stride;
         a.full_frame = k.full_frame;
+        if (pipe && s1 == P.spp && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
         RT_HIP(rt::launch_accumulate(a, st));
+        if (pipe) {
+            RT_HIP(hipEventRecord(sc->ev_free[wb], st));
+            sc->free_valid[wb] = true;
+        }
     }
     return RT_OK;
 }

@@ -846,6 +846,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
 __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 && k.seg_to)
+        for (int c = 0; c < 3; ++c) k.seg_to[c] += k.seg_from[c];
     if (i >= k.n_pixels) return;
     f3 acc;
     if (k.first) acc = mk(0.f, 0.f, 0.f);

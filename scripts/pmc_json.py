@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Condense rocprofv3 --pmc passes of bench.py into the JSON bench.py reads for roofline.traffic.
+
+    python scripts/pmc_json.py <pmc dir with p*/run_counter_collection.csv> <out.json> \
+        [--kernel 'render_kernel<0, 5, false>'] [--config c3] [--camera reference]
+
+Per dispatch of the kernel (mean over dispatches and passes):
+  hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE counts half of the
+                         bytes of wide streaming reads on gfx950, MI355X_MICROARCH.md HBM section)
+  valu_busy            = SQ_INSTS_VALU x 2 cycles / (SIMDs x GRBM_GUI_ACTIVE / 8)
+                         (wave64 VALU issue = 2 cycles; GRBM_GUI_ACTIVE sums the 8 XCDs)
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("root")
+ap.add_argument("out")
+ap.add_argument("--kernel", default="render_kernel<0, 5, false>")
+ap.add_argument("--config", default="c3")
+ap.add_argument("--camera", default="reference")
+ap.add_argument("--traversal", default="cull")
+ap.add_argument("--simds", type=int, default=1024)  # 256 CUs x 4 SIMDs
+a = ap.parse_args()
+
+vals = defaultdict(list)
+for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_counter_collection.csv"))):
+    per = defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        if a.kernel not in r["Kernel_Name"]:
+            continue
+        per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+    by = defaultdict(list)
+    for (_, c), v in per.items():
+        by[c].append(v)
+    for c, v in by.items():
+        vals[c].append(sum(v) / len(v))
+dur = []
+for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_kernel_trace.csv"))):
+    for r in csv.DictReader(open(f)):
+        if a.kernel in r["Kernel_Name"]:
+            dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+m = {c: sum(v) / len(v) for c, v in vals.items()}
+need = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]
+missing = [c for c in need if c not in m]
+if missing:
+    raise SystemExit(f"missing counters {missing} for kernel {a.kernel!r} under {a.root}")
+from bench import WORKLOAD  # noqa: E402
+
+t = sum(dur) / len(dur)
+cycles = m["GRBM_GUI_ACTIVE"] / 8.0
+rec = {
+    "kernel": a.kernel,
+    "config": {"workload": WORKLOAD[a.config], "camera": a.camera, "traversal": a.traversal, "n_gpus": 1},
+    "dispatch_ms": round(t * 1e3, 4),
+    "clock_ghz": round(cycles / t / 1e9, 3),
+    "hbm_bytes_per_launch": int(2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024),
+    "fetch_bytes_corrected": int(2 * m["FETCH_SIZE"] * 1024),
+    "write_bytes": int(m["WRITE_SIZE"] * 1024),
+    "valu_insts": m["SQ_INSTS_VALU"],
+    "valu_busy": round(m["SQ_INSTS_VALU"] * 2.0 / (a.simds * cycles), 4),
+    "valu_lane_ops_per_s": m["SQ_INSTS_VALU"] * 64 / t,
+    "counters": {c: m[c] for c in sorted(m)},
+}
+with open(a.out, "w") as f:
+    json.dump(rec, f, indent=1)
+print(json.dumps({k: v for k, v in rec.items() if k != "counters"}))

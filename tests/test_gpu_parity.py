@@ -283,3 +283,30 @@ def test_chunking_and_passes_bit_exact(chunk, budget_samples, shade_lds, monkeyp
     got, st = rt.render_f32((s, m), p)
     _bits_equal(got, want)
     assert st.segments == want_seg
+
+
+@pytest.mark.gpu
+def test_frames_in_flight_match_serial(monkeypatch):
+    """Consecutive rt_render_device calls on one scene overlap (render kernels on internal
+    streams, double-buffered workspaces); every frame must still equal its serial render,
+    with different cameras, spp and row partitions back to back and no sync between calls."""
+    import torch
+    s, m = G.scene("huge")
+    W, H = 48, 32
+    jobs = [(rt.make_params(W, H, 8, 64, 1), O.camera_default(W, H, abi.RT_CAMERA_REFERENCE), H),
+            (rt.make_params(W, H, 5, 64, 2), O.camera_default(W, H, abi.RT_CAMERA_CORRECTED), H),
+            (rt.make_params(W, H, 12, 64, 3, row_offset=1, row_stride=2), O.camera_default(W, H, 0), H // 2),
+            (rt.make_params(W, H, 4, 7, 4), O.camera_default(W, H, abi.RT_CAMERA_CORRECTED), H)]
+    ds = rt.DeviceScene((s, m))
+    stream = torch.cuda.current_stream().cuda_stream
+    outs, segs = [], []
+    for p, cam, rows in jobs * 2:
+        outs.append(torch.empty((rows, W, 3), dtype=torch.float32, device="cuda"))
+        segs.append(torch.zeros(3, dtype=torch.int64, device="cuda"))
+        ds.render(cam, p, outs[-1].data_ptr(), stream, segs[-1].data_ptr())
+    torch.cuda.synchronize()
+    for i, (p, cam, rows) in enumerate(jobs * 2):
+        want, want_seg = O.render_f32(s, m, cam, p)
+        _bits_equal(outs[i].cpu().numpy(), want)
+        assert int(segs[i][0]) == want_seg
+    ds.close()

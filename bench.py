@@ -38,6 +38,8 @@ CONFIGS = {
     "c4": ("huge", 3840, 2160, 256, 64),
     "c5": ("huge", 1280, 720, 1024, 64),
     "c1": ("simple", 200, 100, 1, 64),
+    # the reference's CUDA variant (cuda_impl.cu): its scene, camera, 48 spp, 32 bounces
+    "cuda": ("cuda", 1280, 720, 48, 32),
 }
 WORKLOAD = {
     "c3": "huge-scene 1280x720x128spp (BASELINE config 3)",
@@ -45,6 +47,7 @@ WORKLOAD = {
     "c4": "huge-scene 3840x2160x256spp (config 4)",
     "c5": "huge-scene 1280x720x1024spp (config 5)",
     "c1": "simple-scene 200x100x1spp (config 1)",
+    "cuda": "cuda_impl preset: its 5-sphere scene 1280x720x48spp depth 32 (RT_FLAG_CUDA_COMPAT)",
 }
 
 
@@ -90,6 +93,17 @@ def cpu_baseline(cfg, camera, seed, rows, threads):
     threads = threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
     exe = os.path.join(REPO, "oracle", "_ref", "ref_harness_pcg")
     sample = f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, {scene} scene, {camera} camera"
+    if scene == "cuda":  # the CUDA variant has no CPU path in the reference: the restatement
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_binding as O
+        import raytracinginoneweekend_amd as rt
+        s, m = rt.cuda_scene_arrays()
+        p = O.make_params(W, H, spp, depth, 0, 0, step, nrows, flags=rt.abi.RT_FLAG_CUDA_COMPAT)
+        t0 = time.perf_counter()
+        O.render_cuda_compat(s, m, rt.Camera.cuda(W, H).c, p, threads=threads)
+        sec = time.perf_counter() - t0
+        return {"value": round(W * nrows * spp / sec / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+                "sample": f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, cuda_impl preset; {sec:.1f} s wall"}
     if os.path.exists(exe):
         cmd = [exe, "--scene", scene, "--scene-seed", "1234", "--w", str(W), "--h", str(H), "--spp", str(spp),
                "--depth", str(depth), "--seed", str(seed), "--camera", camera, "--row0", "0",
@@ -132,14 +146,16 @@ def main():
 
     import raytracinginoneweekend_amd as rt
     scene_name, W, H, spp, depth = CONFIGS[args.config]
-    arrays = rt.huge_scene_arrays(1234) if scene_name == "huge" else rt.simple_scene_arrays()
+    compat = scene_name == "cuda"
+    arrays = rt.huge_scene_arrays(1234) if scene_name == "huge" else (
+        rt.cuda_scene_arrays() if compat else rt.simple_scene_arrays())
     n_spheres = len(arrays[0])
     mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
-    cam = rt.Camera.default(W, H, mode)
+    cam = rt.Camera.cuda(W, H) if compat else rt.Camera.default(W, H, mode)
     from raytracinginoneweekend_amd.rowtiles import FrameGather, rank_params
     params = rank_params(W, H, spp, world, rank, max_depth=depth, seed=args.seed,
                          scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast",
-                         brute_force=args.traversal == "brute")
+                         brute_force=args.traversal == "brute", cuda_compat=compat)
     rows = params.num_rows
     dev = torch.device("cuda", local)
     ds = rt.DeviceScene(arrays, device=local)
@@ -219,7 +235,8 @@ def main():
             "data": "synthetic (reference huge scene, std::mt19937 seed 1234; per-sample PCG32 seed %d)" % args.seed,
             "config": {"workload": WORKLOAD[args.config], "scene": f"{scene_name} ({n_spheres} spheres)",
                        "width": W, "height": H, "spp": spp, "max_depth": depth, "camera": args.camera,
-                       "kernel": ("fast (FMA, stated tolerance)" if args.variant == "fast" else f"{args.variant} (bit-exact)")
+                       "kernel": "compat_kernel (cuda_impl.cu semantics, bit-exact vs its restatement)" if compat else
+                       ("fast (FMA, stated tolerance)" if args.variant == "fast" else f"{args.variant} (bit-exact)")
                        + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
             "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
             "frame_latency_ms": round(latency * 1e3, 3),
@@ -227,7 +244,7 @@ def main():
             "segments_per_primary": round(segments_all / primaries, 4),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                         "kernel": "render_kernel", "kernel_avg_ms": round(k_avg_ms, 3),
+                         "kernel": "compat_kernel" if compat else "render_kernel", "kernel_avg_ms": round(k_avg_ms, 3),
                          "flop_per_launch": flop_per_launch, "work": "executed sphere+box tests",
                          "brute_force_equiv_tflops": round(brute_equiv, 2)},
             "tests_per_segment": round(sph_tests / max(segments, 1), 2),

@@ -94,7 +94,9 @@ enum rt_flags {
     RT_FLAG_FULL_FRAME = 1u << 0, /* write rows at their global position             */
     RT_FLAG_FAST_MATH = 1u << 1,  /* FMA-contracted kernel, stated tolerance          */
     RT_FLAG_SCALAR_SCENE = 1u << 2, /* A/B: brute force, spheres via the scalar cache   */
-    RT_FLAG_BRUTE_FORCE = 1u << 3   /* test every sphere (no cluster culling); same bits */
+    RT_FLAG_BRUTE_FORCE = 1u << 3,  /* test every sphere (no cluster culling); same bits */
+    RT_FLAG_CUDA_COMPAT = 1u << 4   /* semantics of the reference's CUDA variant instead of its
+                                       CPU path: src/CUDA/cuda_impl.cu (see rt_render_cuda_impl) */
 };
 typedef struct rt_params {
     uint32_t width, height;
@@ -128,6 +130,12 @@ int rt_camera_default(uint32_t width, uint32_t height, uint32_t mode, rt_camera 
 /* Simple scene, src/main.cxx:120-129: 5 spheres, 4 materials.                          */
 int rt_scene_simple(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres,
                     rt_material *materials, uint32_t material_cap, uint32_t *n_materials);
+/* The CUDA variant's hardcoded scene, src/CUDA/cuda_impl.cu:425-437: 5 spheres, 4 materials. */
+int rt_scene_cuda(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres,
+                  rt_material *materials, uint32_t material_cap, uint32_t *n_materials);
+/* The CUDA variant's camera, src/CUDA/cuda_impl.cu:371-375 (origin 0, look -z, vFOV 88,
+ * focus 1; its rays carry no lens offset, camera.hxx:48-50).                            */
+int rt_camera_cuda(uint32_t width, uint32_t height, rt_camera *out);
 /* Huge random scene: simple scene + the generator of src/main.cxx:131-177 driven by
  * std::mt19937{seed} (the reference seeds from std::random_device). Namespace typo
  * fixed; a "type 3" draw pushes no material (as shipped), so such a sphere aliases the
@@ -154,6 +162,15 @@ int rt_render_multi_f32(const rt_sphere *spheres, uint32_t n_spheres,
                         const rt_material *materials, uint32_t n_materials,
                         const rt_camera *camera, const rt_params *params, int ngpu,
                         float *rgb_out, rt_stats *stats);
+
+/* The literal replacement of the reference's accelerated entry point
+ *     void cuda_impl(uint32_t width, uint32_t height, std::vector<u8vec3> &image_texels)
+ * (src/main.cxx:18, defined src/CUDA/cuda_impl.cu:384-453): its scene and camera, 48 spp,
+ * 32 bounces, one xorshift32 engine per pixel seeded with the pixel index, gamma 1/2.2 and
+ * (uint8)(255 c). rgb_out: width*height*3 bytes, row 0 = top. Synchronous.
+ * With RT_FLAG_CUDA_COMPAT in rt_params any scene/camera/spp/depth renders with those
+ * semantics (seed is added to the pixel index; the camera's lens radius is not used).   */
+int rt_render_cuda_impl(uint32_t width, uint32_t height, uint8_t *rgb_out);
 
 /* ---- device-resident API (inputs resident in HBM, async on a caller stream) -------- */
 typedef struct rt_scene rt_scene;

@@ -252,9 +252,136 @@ inline std::uint32_t rows_of(const rt_params &p)
     return p.row_offset >= p.height ? 0 : (p.height - p.row_offset + st - 1) / st;
 }
 
+// ---- the reference's CUDA variant, src/CUDA/cuda_impl.cu (RT_FLAG_CUDA_COMPAT) ----------
+// Parity unpinned against the variant itself: it needs nvcc + thrust, absent here; this is a
+// restatement from its source, line by line, with every binary32 op separately rounded.
+struct xorshift32 {                                                             // cuda_impl.cu:13-41
+    std::uint32_t s;
+    float generate()
+    {
+        s ^= (s << 13);
+        s ^= (s >> 17);
+        s ^= (s << 5);
+        return static_cast<float>(s) * (1.f / 4294967296.f);
+    }
+    v3 random_in_unit_sphere()                                                  // :43-56
+    {
+        v3 v;
+        do {
+            float x = generate() * 2.f - 1.f;
+            float y = generate() * 2.f - 1.f;
+            float z = generate() * 2.f - 1.f;
+            v = mk(x, y, z);
+        } while (length(v) > 1.f && s != 0u);  // a zero state never leaves 0: the variant would spin
+        return v;
+    }
+};
+
+// :131-186: shrinking t_max with strict comparisons; the lowest index wins a tie
+inline hit cu_hit_world(const scene &sc, const ray &r)
+{
+    hit best{}; best.ok = false;
+    float tmax = FLT_MAX;
+    for (std::uint32_t i = 0; i < sc.n; ++i) {
+        hit h;
+        if (intersect(r, sc.s[i], .008f, tmax, h)) { best = h; tmax = h.t; }
+    }
+    return best;
+}
+
+// :288-324
+inline v3 cu_color(const scene &sc, xorshift32 &g, ray r, std::uint32_t bounces, std::uint64_t &segments)
+{
+    v3 atten = mk(1.f, 1.f, 1.f);
+    for (std::uint32_t b = 0; b < bounces; ++b) {
+        ++segments;
+        hit h = cu_hit_world(sc, r);
+        if (!h.ok) return mulv(background(normalize(r.d).y * .5f + .5f), atten);   // :320
+        const rt_material &m = sc.m[h.mat];
+        v3 albedo = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+        ray nr;
+        bool valid = true;
+        if (m.kind == RT_LAMBERT) {                                                // :197-206
+            v3 rd = normalize(g.random_in_unit_sphere());
+            nr = {h.p, add(h.n, rd)};
+        } else if (m.kind == RT_METAL) {                                           // :208-222
+            v3 refl = reflect(normalize(r.d), h.n);
+            v3 rd = normalize(g.random_in_unit_sphere());
+            nr = {h.p, add(refl, muls(rd, m.param))};
+            valid = dot(nr.d, h.n) > 0.f;
+        } else {                                                                   // :224-256
+            v3 ud = normalize(r.d);
+            v3 outward = neg(h.n);
+            float ri = m.param;
+            float cosv = dot(ud, h.n);
+            if (cosv <= 0.f) {
+                outward = muls(outward, -1.f);
+                ri = 1.f / ri;
+                cosv *= -1.f;
+            }
+            v3 refr = refract(ud, outward, ri);
+            float prob = 1.f;
+            if (length(refr) > 0.f) prob = schlick(ri, cosv);
+            if (g.generate() < prob) nr = {h.p, reflect(ud, h.n)};
+            else nr = {h.p, refr};
+        }
+        if (!valid) return mk(0.f, 0.f, 0.f);                                      // :308
+        r = nr;
+        atten = mulv(atten, albedo);                                               // :303-305
+    }
+    return mk(0.f, 0.f, 0.f);
+}
+
 } // namespace
 
 extern "C" {
+
+// cuda::data::render (:340-355) for every pixel of the rows of `params`; camera rays without a
+// lens offset (camera.hxx:48-50); engine state = pixel index x + y W + seed (:408-413).
+int oracle_render_cuda_compat(const rt_sphere *spheres, uint32_t n, const rt_material *mats, uint32_t nm,
+                              const rt_camera *camera, const rt_params *params, int threads, float *out,
+                              uint64_t *segments_out)
+{
+    if (!spheres || !mats || !camera || !params || !out || params->spp == 0) return RT_ERR_INVALID;
+    const rt_params p = *params;
+    const scene sc{spheres, n, mats, nm};
+    const cam c = to_cam(camera);
+    const std::uint32_t nrows = rows_of(p), stride = p.row_stride ? p.row_stride : 1;
+    const bool full = p.flags & RT_FLAG_FULL_FRAME;
+    if (threads < 1) threads = 1;
+    std::vector<std::uint64_t> segs(threads, 0);
+    auto worker = [&](int tid) {
+        std::uint64_t seg = 0;
+        for (std::uint32_t i = tid; i < nrows; i += threads) {
+            const std::uint32_t y = p.row_offset + i * stride;
+            for (std::uint32_t x = 0; x < p.width; ++x) {
+                xorshift32 g{x + y * p.width + static_cast<std::uint32_t>(p.seed)};
+                v3 col = mk(0.f, 0.f, 0.f);
+                for (std::uint32_t s = 0; s < p.spp; ++s) {
+                    float u = (static_cast<float>(x) + g.generate()) / static_cast<float>(p.width);
+                    float v = (static_cast<float>(y) + g.generate()) / static_cast<float>(p.height);
+                    ray r{c.origin, add(add(c.llc, muls(c.hor, u)), muls(c.ver, 1.f - v))};
+                    col = add(col, cu_color(sc, g, r, p.max_depth, seg));
+                }
+                col = divs(col, static_cast<float>(p.spp));
+                const std::size_t row = full ? y : i;
+                float *o = out + (row * p.width + x) * 3;
+                o[0] = col.x; o[1] = col.y; o[2] = col.z;
+            }
+        }
+        segs[tid] = seg;
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(worker, t);
+    worker(0);
+    for (auto &t : pool) t.join();
+    if (segments_out) {
+        std::uint64_t s = 0;
+        for (auto v : segs) s += v;
+        *segments_out = s;
+    }
+    return RT_OK;
+}
 
 // Per-sample PCG streams (rng_mode 0, the GPU contract) or the reference's shared
 // mt19937 streams (rng_mode 1; data seeded `seed`, camera `seed+1`, single thread).

@@ -21,6 +21,7 @@ RT_FLAG_FULL_FRAME = 1 << 0
 RT_FLAG_FAST_MATH = 1 << 1
 RT_FLAG_SCALAR_SCENE = 1 << 2
 RT_FLAG_BRUTE_FORCE = 1 << 3
+RT_FLAG_CUDA_COMPAT = 1 << 4  # semantics of src/CUDA/cuda_impl.cu
 
 
 class RtSphere(C.Structure):

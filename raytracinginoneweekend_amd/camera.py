@@ -29,6 +29,14 @@ class Camera:
         check(lib().rt_camera_default(width, height, mode, C.byref(self.c)))
         return self
 
+    @classmethod
+    def cuda(cls, width, height):
+        """The reference CUDA variant's camera (src/CUDA/cuda_impl.cu:371-375)."""
+        self = cls.__new__(cls)
+        self.c = abi.RtCamera()
+        check(lib().rt_camera_cuda(width, height, C.byref(self.c)))
+        return self
+
     @property
     def mode(self):
         return self.c.mode

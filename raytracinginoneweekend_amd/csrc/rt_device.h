@@ -91,6 +91,21 @@ struct KAccum {
     unsigned long long *seg_to;
 };
 
+// RT_FLAG_CUDA_COMPAT: the semantics of the reference's CUDA variant (src/CUDA/cuda_impl.cu),
+// see compat_kernel. One lane owns one pixel (its xorshift32 engine is sequential over the
+// pixel's samples), lanes refill from a per-wave cursor over 64-pixel chunks.
+struct KCompat {
+    float org[3], llc[3], hor[3], ver[3];
+    uint32_t W, H, spp, max_depth;
+    uint32_t row_offset, row_stride, num_rows, full_frame;
+    uint32_t seed;           // added to the pixel index x + y W (the reference: 0)
+    uint32_t n_spheres, n_pixels, n_chunks;
+    const float4 *shade;     // per sphere: {cx, cy, cz, r}, {albedo, param}, then n kind bytes
+    float *out;
+    uint32_t *ctr;
+    unsigned long long *segments;  // optional [3]: segments, sphere tests, 0
+};
+
 // queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise
 constexpr uint32_t kQueueStride = 64;
 

@@ -27,6 +27,8 @@ namespace rt {
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream);
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
+hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream);
+hipError_t occupancy_compat(int *blocks_per_cu);
 hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_t stream);
 } // namespace rt
 
@@ -61,7 +63,9 @@ hv hnorm(hv a)
 hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x}; }
 
 constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 GiB)
-constexpr size_t kCtrWords = 16 * rt::kQueueStride + 16;  // 2 x 8 queue lines + 2 x 4 u64 segment counters
+// 2 x 8 queue lines, 2 x 4 u64 segment counters, then the compat kernel's pixel counter
+constexpr size_t kCtrWords = 17 * rt::kQueueStride + 16;
+constexpr size_t kCompatCtr = 16 * rt::kQueueStride + 16;
 
 // RT_SLOT_BUDGET_BYTES lowers the per-pass slot workspace (tests force multi-pass renders).
 uint64_t slot_budget()
@@ -166,6 +170,17 @@ int rt_camera_init(const float position[3], const float lookat[3], const float u
 }
 
 // src/main.cxx:179-183
+int rt_camera_cuda(uint32_t width, uint32_t height, rt_camera *out)
+{
+    // cuda_impl.cu:371-375: position 0, look (0, 0, -1), up y, vFOV 88, aperture .0625, focus 1;
+    // camera::ray has no lens offset under CUDA_IMPL (camera.hxx:48-50), and with the origin at
+    // 0 the missing "- origin" does not matter
+    if (!width || !height) return fail(RT_ERR_INVALID, "rt_camera_cuda: zero size");
+    const float pos[3] = {0.f, 0.f, 0.f}, look[3] = {0.f, 0.f, -1.f}, up[3] = {0.f, 1.f, 0.f};
+    return rt_camera_init(pos, look, up, static_cast<float>(width) / static_cast<float>(height), 88.f, .0625f, 1.f,
+                          RT_CAMERA_REFERENCE, out);
+}
+
 int rt_camera_default(uint32_t width, uint32_t height, uint32_t mode, rt_camera *out)
 {
     if (!width || !height) return fail(RT_ERR_INVALID, "rt_camera_default: zero size");
@@ -199,6 +214,18 @@ struct scene_builder {
     // src/main.cxx:131-177 (namespace typo fixed). Draw order: type, center.x, center.z, then
     // the material's draws; a type-3 sphere pushes no material, so it shares the index of the
     // next pushed one and trailing ones are resolved by default materials (lambert, albedo 1).
+    void cuda_variant()  // src/CUDA/cuda_impl.cu:425-437
+    {
+        mat(RT_LAMBERT, static_cast<float>(.1), static_cast<float>(.2), static_cast<float>(.5), 0.f);
+        mat(RT_METAL, static_cast<float>(.8), static_cast<float>(.6), static_cast<float>(.2), 0.f);
+        mat(RT_DIELECTRIC, 1.f, 1.f, 1.f, 1.5f);
+        mat(RT_LAMBERT, static_cast<float>(.64), static_cast<float>(.8), static_cast<float>(.0), 0.f);
+        sph(0.f, 0.f, -1.f, .5f, 0);
+        sph(0.f, -100.5f, -1.f, 100.f, 3);
+        sph(1.f, 0.f, -1.f, .5f, 1);
+        sph(-1.f, 0.f, -1.f, .5f, 2);
+        sph(-1.f, 0.f, -1.f, -.499f, 2);
+    }
     void huge(uint32_t seed)
     {
         simple();
@@ -455,7 +482,7 @@ int check_params(const rt_params *p)
     const uint32_t rows = rows_of(*p);
     if (rows && static_cast<uint64_t>(p->row_offset) + static_cast<uint64_t>(rows - 1) * st >= p->height)
         return fail(RT_ERR_INVALID, "params: rows exceed the image height");
-    if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE | RT_FLAG_BRUTE_FORCE))
+    if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE | RT_FLAG_BRUTE_FORCE | RT_FLAG_CUDA_COMPAT))
         return fail(RT_ERR_INVALID, "params: unknown flag");
     return RT_OK;
 }
@@ -518,6 +545,16 @@ uint32_t root_box_env()
 
 
 
+} // namespace
+
+struct rt_scene;
+namespace {
+
+// RT_FLAG_CUDA_COMPAT: the reference's CUDA variant semantics (compat_kernel), on the caller
+// stream, spheres read from the index-ordered shading records of the brute-force blob.
+int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, float *d_rgb, hipStream_t st,
+                  uint64_t *d_segments);
+
 // RT_PIPELINE=0 runs the render kernels on the caller stream (no frames in flight).
 bool pipeline_env()
 {
@@ -569,6 +606,14 @@ int rt_scene_simple(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres
 {
     scene_builder b;
     b.simple();
+    return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
+}
+
+int rt_scene_cuda(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres, rt_material *materials,
+                  uint32_t material_cap, uint32_t *n_materials)
+{
+    scene_builder b;
+    b.cuda_variant();
     return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
 }
 
@@ -710,6 +755,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     const rt_params P = *params;
     hipStream_t st = static_cast<hipStream_t>(stream);
     RT_HIP(hipSetDevice(sc->device));
+
+    if (P.flags & RT_FLAG_CUDA_COMPAT) return render_compat(sc, camera, P, d_rgb, st, d_segments);
 
     rt::KParams k{};
     for (int c = 0; c < 3; ++c) {
@@ -878,6 +925,67 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     }
     return RT_OK;
 }
+
+namespace {
+int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, float *d_rgb, hipStream_t st,
+                  uint64_t *d_segments)
+{
+    rt::KCompat k{};
+    for (int c = 0; c < 3; ++c) {
+        k.org[c] = camera->origin[c];
+        k.llc[c] = camera->lower_left_corner[c];
+        k.hor[c] = camera->horizontal[c];
+        k.ver[c] = camera->vertical[c];
+    }
+    k.W = P.width;
+    k.H = P.height;
+    k.spp = P.spp;
+    k.max_depth = P.max_depth;
+    k.row_offset = P.row_offset;
+    k.row_stride = P.row_stride ? P.row_stride : 1;
+    k.num_rows = rows_of(P);
+    k.full_frame = (P.flags & RT_FLAG_FULL_FRAME) ? 1u : 0u;
+    k.seed = static_cast<uint32_t>(P.seed);
+    k.n_spheres = sc->n_spheres;
+    const uint64_t n_pixels = static_cast<uint64_t>(P.width) * k.num_rows;
+    if (n_pixels == 0) return RT_OK;
+    if (n_pixels >= (1ull << 31)) return fail(RT_ERR_INVALID, "rt_render_device: more than 2^31 pixels in one call");
+    k.n_pixels = static_cast<uint32_t>(n_pixels);
+    k.n_chunks = (k.n_pixels + 63u) / 64u;
+    k.shade = reinterpret_cast<const float4 *>(sc->blob[0]) + sc->shade_offset[0];
+    k.out = d_rgb;
+    k.ctr = sc->queue_ctr + kCompatCtr;
+    k.segments = reinterpret_cast<unsigned long long *>(d_segments);
+    int occ = 0;
+    RT_HIP(rt::occupancy_compat(&occ));
+    const uint32_t grid = static_cast<uint32_t>(
+        std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(std::max(occ, 1)) * sc->cu_count, (n_pixels + 255u) / 256u)));
+    const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
+    ++sc->calls;
+    RT_HIP(hipMemsetAsync(k.ctr, 0, sizeof(uint32_t), st));
+    RT_HIP(hipEventRecord(sc->ev_begin[ring], st));
+    RT_HIP(rt::launch_compat(k, grid, st));
+    RT_HIP(hipEventRecord(sc->ev_end[ring], st));
+    return RT_OK;
+}
+} // namespace
+
+extern "C" {
+
+int rt_render_cuda_impl(uint32_t width, uint32_t height, uint8_t *rgb_out)
+{
+    if (!rgb_out) return fail(RT_ERR_INVALID, "rt_render_cuda_impl: null output");
+    rt_sphere s[8];
+    rt_material m[8];
+    uint32_t ns = 0, nm = 0;
+    if (int rc = rt_scene_cuda(s, 8, &ns, m, 8, &nm); rc) return rc;
+    rt_camera cam;
+    if (int rc = rt_camera_cuda(width, height, &cam); rc) return rc;
+    rt_params p{width, height, 48, 32, 0, 0, 1, 0, RT_FLAG_CUDA_COMPAT};  // cuda_impl.cu:62-63
+    return rt_render_rgb8(s, ns, m, nm, &cam, &p, rgb_out, nullptr);
+}
+
+} // extern "C"
 
 int rt_scene_kernel_times(rt_scene *sc, uint32_t max, float *ms, uint32_t *n)
 {

@@ -842,6 +842,185 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     }
 }
 
+// ---- the reference's CUDA variant (RT_FLAG_CUDA_COMPAT) -----------------------------------
+// src/CUDA/cuda_impl.cu as written, every binary32 op separately rounded in its order:
+//   engine    xorshift32 per pixel, seeded with the pixel index (:16-41, :408-413); generate()
+//             = float(x) * 2^-32 without a clamp (:37-41)
+//   sampling  u = (float(x) + g) / W, v = (float(y) + g) / H, samples summed in order, / spp
+//             (:342-351); camera without a lens offset (camera.hxx:48-50)
+//   color     32 bounces by default (:63), sky mix(1, (.5,.7,1), .5 y + .5) * attenuation (:310)
+//   hit       shrinking t_max, strict '<', lowest index wins ties (:131-186)
+//   lambert   target = n + normalize(rius) (:197-206); metal reflect(unit d, n) +
+//             normalize(rius) * roughness, absorbed unless dot > 0 (:208-222); dielectric as
+//             the CPU path (:224-256), Schlick in double like raytracer.hxx:45-50
+// An engine whose state is 0 stays 0 (xorshift's fixed point) and the reference's rejection
+// loop would never end; here such a loop exits after one draw (only a seed that makes a
+// pixel's state 0 can reach it: pixel 0 with seed 0, whose rays the default camera sends to
+// the sky).
+__device__ __forceinline__ float xs_gen(uint32_t &st)
+{
+    st ^= st << 13;
+    st ^= st >> 17;
+    st ^= st << 5;
+    return (float)st * (1.f / 4294967296.f);
+}
+__device__ __forceinline__ f3 xs_unit_sphere(uint32_t &st)  // cuda_impl.cu:43-56
+{
+    f3 v;
+    do {
+        const float x = xs_gen(st) * 2.f - 1.f;
+        const float y = xs_gen(st) * 2.f - 1.f;
+        const float z = xs_gen(st) * 2.f - 1.f;
+        v = mk(x, y, z);
+    } while (v.x * v.x + v.y * v.y + v.z * v.z > 0x1.000002p+0f && st != 0u);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void compat_kernel(const KCompat p)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const float4 *shade = p.shade;
+    const uint8_t *kinds = reinterpret_cast<const uint8_t *>(shade + 2 * p.n_spheres);
+    const f3 org = mk(p.org[0], p.org[1], p.org[2]), llc = mk(p.llc[0], p.llc[1], p.llc[2]);
+    const f3 hor = mk(p.hor[0], p.hor[1], p.hor[2]), ver = mk(p.ver[0], p.ver[1], p.ver[2]);
+    const float fW = (float)p.W, fH = (float)p.H;
+
+    uint32_t cnext = 0, cend = 0;
+    bool exhausted = false, alive = false, fresh = false;
+    uint32_t i = 0, x = 0, y = 0, s = 0, depth = 0, rng = 0;
+    f3 o = mk(0.f, 0.f, 0.f), d = o, att = o, col = o;
+    uint32_t segs = 0, tests = 0;
+    for (;;) {
+        // refill: idle lanes take the next pixels of the wave's chunk (64 pixels per atomic)
+        uint64_t need = __ballot(!alive);
+        while (need && !exhausted) {
+            if (cnext >= cend) {
+                uint32_t c = 0;
+                if (lane == 0) c = atomicAdd(p.ctr, 1u);
+                c = __builtin_amdgcn_readfirstlane(c);
+                if (c >= p.n_chunks) { exhausted = true; break; }
+                cnext = c * 64u;
+                cend = min(cnext + 64u, p.n_pixels);
+            }
+            const uint32_t avail = cend - cnext;
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            if (!alive && rank < avail) {
+                i = cnext + rank;
+                const uint32_t rr = i / p.W;
+                x = i - rr * p.W;
+                y = p.row_offset + rr * p.row_stride;
+                rng = x + y * p.W + p.seed;                 // cuda_impl.cu:408-413
+                s = 0;
+                col = mk(0.f, 0.f, 0.f);
+                alive = fresh = true;
+            }
+            cnext += min((uint32_t)__popcll(need), avail);
+            need = __ballot(!alive);
+        }
+        if (__ballot(alive) == 0) break;
+        if (!alive) continue;
+        if (fresh) {                                        // cuda_impl.cu:345-349
+            const float u = ((float)x + xs_gen(rng)) / fW;
+            const float v = ((float)y + xs_gen(rng)) / fH;
+            o = org;
+            d = (llc + hor * u) + ver * (1.f - v);
+            att = mk(1.f, 1.f, 1.f);
+            depth = 0;
+            fresh = false;
+        }
+        bool done = false;
+        f3 c = mk(0.f, 0.f, 0.f);
+        if (depth >= p.max_depth) {
+            done = true;                                    // :320
+        } else {
+            ++segs;
+            // hit_world :171-186
+            const float a = d.x * d.x + d.y * d.y + d.z * d.z;
+            float tmax = RT_TMAX;
+            uint32_t ib = 0xffffffffu;
+            for (uint32_t k = 0; k < p.n_spheres; ++k) {
+                const float4 sf = shade[2 * k];
+                const float ocx = o.x - sf.x, ocy = o.y - sf.y, ocz = o.z - sf.z;
+                const float b = ocx * d.x + ocy * d.y + ocz * d.z;
+                const float cc = ocx * ocx + ocy * ocy + ocz * ocz - sf.w * sf.w;
+                const float disc = b * b - a * cc;
+                if (disc > 0.f) {
+                    const float q = sqrtf(disc);
+                    float t = (-b - q) / a;
+                    if (!(t < tmax && t > RT_TMIN)) t = (-b + q) / a;
+                    if (t < tmax && t > RT_TMIN) { tmax = t; ib = k; }
+                }
+            }
+            tests += p.n_spheres;
+            ++depth;
+            if (ib == 0xffffffffu) {
+                const float tt = normalize(d).y * .5f + .5f;   // :310
+                c = (mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt) * att;
+                done = true;
+            } else {
+                const float4 sf = shade[2 * ib], md = shade[2 * ib + 1];
+                const uint32_t kind = kinds[ib];
+                const f3 hp = o + d * tmax;
+                const f3 hn = (hp - mk(sf.x, sf.y, sf.z)) / sf.w;
+                bool valid = true;
+                f3 nd;
+                if (kind == 0u) {                            // :197-206
+                    nd = hn + normalize(xs_unit_sphere(rng));
+                } else if (kind == 1u) {                     // :208-222
+                    const f3 refl = reflect(normalize(d), hn);
+                    nd = refl + normalize(xs_unit_sphere(rng)) * md.w;
+                    valid = dot(nd, hn) > 0.f;
+                } else {                                     // :224-256
+                    const f3 ud = normalize(d);
+                    f3 outward = mk(-hn.x, -hn.y, -hn.z);
+                    float ri = md.w;
+                    float cosv = dot(ud, hn);
+                    if (cosv <= 0.f) {
+                        outward = outward * -1.f;
+                        ri = 1.f / ri;
+                        cosv *= -1.f;
+                    }
+                    const f3 refr = refract(ud, outward, ri);
+                    float prob = 1.f;
+                    if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick(ri, cosv);
+                    nd = xs_gen(rng) < prob ? reflect(ud, hn) : refr;
+                }
+                if (!valid) {
+                    done = true;                             // :308
+                } else {
+                    o = hp;
+                    d = nd;
+                    att = att * mk(md.x, md.y, md.z);        // :303-305
+                    if (depth >= p.max_depth) done = true;   // :316
+                }
+            }
+        }
+        if (done) {
+            col = col + c;                                  // :350
+            if (++s == p.spp) {
+                col = col / (float)p.spp;                   // :353
+                const uint32_t row = p.full_frame ? y : i / p.W;
+                float *dst = p.out + ((size_t)row * p.W + x) * 3u;
+                dst[0] = col.x;
+                dst[1] = col.y;
+                dst[2] = col.z;
+                alive = false;
+            } else {
+                fresh = true;
+            }
+        }
+    }
+    if (p.segments) {
+        const unsigned long long cv[2] = {segs, tests};
+        for (int k = 0; k < 2; ++k) {
+            unsigned long long v = cv[k];
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) atomicAdd(p.segments + k, v);
+        }
+    }
+}
+
 // ---- ordered accumulation of the slots, average, optional gamma/u8 --------------------
 __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
 {
@@ -940,6 +1119,18 @@ hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t ld
     const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
+}
+
+hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream)
+{
+    hipLaunchKernelGGL(compat_kernel, dim3(grid), dim3(256), 0, stream, k);
+    return hipGetLastError();
+}
+
+hipError_t occupancy_compat(int *blocks_per_cu)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, reinterpret_cast<const void *>(&compat_kernel),
+                                                        256, 0);
 }
 
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream)

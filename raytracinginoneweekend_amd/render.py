@@ -15,9 +15,10 @@ from .camera import Camera
 
 
 def make_params(width, height, spp, max_depth=64, seed=1234, row_offset=0, row_stride=1, num_rows=0,
-                full_frame=False, scalar_scene=False, fast_math=False, brute_force=False):
+                full_frame=False, scalar_scene=False, fast_math=False, brute_force=False, cuda_compat=False):
     flags = (abi.RT_FLAG_FULL_FRAME if full_frame else 0) | (abi.RT_FLAG_SCALAR_SCENE if scalar_scene else 0) \
-        | (abi.RT_FLAG_FAST_MATH if fast_math else 0) | (abi.RT_FLAG_BRUTE_FORCE if brute_force else 0)
+        | (abi.RT_FLAG_FAST_MATH if fast_math else 0) | (abi.RT_FLAG_BRUTE_FORCE if brute_force else 0) \
+        | (abi.RT_FLAG_CUDA_COMPAT if cuda_compat else 0)
     return abi.RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, num_rows, flags)
 
 
@@ -70,6 +71,14 @@ def render_multi_f32(scene, params, ngpu=0, camera=None):
                                     abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), C.byref(_cam(camera, params)),
                                     C.byref(params), ngpu, abi.ptr(out, C.POINTER(C.c_float)), C.byref(st)))
     return out, st
+
+
+def render_cuda_impl(width, height):
+    """cuda_impl(width, height, image_texels) (src/main.cxx:18, src/CUDA/cuda_impl.cu:384-453):
+    the CUDA variant's scene, camera, 48 spp and 32 bounces; u8 RGB (height, width, 3)."""
+    out = np.zeros((height, width, 3), dtype=np.uint8)
+    check(lib().rt_render_cuda_impl(width, height, abi.ptr(out, C.POINTER(C.c_uint8))))
+    return out
 
 
 class DeviceScene:

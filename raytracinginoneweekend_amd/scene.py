@@ -125,6 +125,11 @@ def huge_scene_arrays(seed=1234):
     return _from_c(lib().rt_scene_huge, seed)
 
 
+def cuda_scene_arrays():
+    """The reference CUDA variant's hardcoded scene (src/CUDA/cuda_impl.cu:425-437)."""
+    return _from_c(lib().rt_scene_cuda)
+
+
 def simple_scene():
     return RaytracerData.from_arrays(*simple_scene_arrays())
 

@@ -29,6 +29,11 @@ def lib():
             C.POINTER(abi.RtSphere), C.c_uint32, C.POINTER(abi.RtMaterial), C.c_uint32,
             C.POINTER(abi.RtCamera), C.POINTER(abi.RtParams), C.c_int, C.c_int,
             C.POINTER(C.c_float), C.POINTER(C.c_uint64)]
+        L.oracle_render_cuda_compat.restype = C.c_int
+        L.oracle_render_cuda_compat.argtypes = [
+            C.POINTER(abi.RtSphere), C.c_uint32, C.POINTER(abi.RtMaterial), C.c_uint32,
+            C.POINTER(abi.RtCamera), C.POINTER(abi.RtParams), C.c_int, C.POINTER(C.c_float),
+            C.POINTER(C.c_uint64)]
         L.oracle_epilogue_rgb8.restype = None
         L.oracle_epilogue_rgb8.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.c_uint64]
         L.oracle_camera_init.restype = C.c_int
@@ -75,6 +80,22 @@ def render_f32(spheres, materials, camera, params, rng_mode=0, threads=None):
                                  abi.ptr(materials, C.POINTER(abi.RtMaterial)), len(materials),
                                  C.byref(camera), C.byref(params), rng_mode, threads,
                                  abi.ptr(out, C.POINTER(C.c_float)), C.byref(seg))
+    assert rc == 0, rc
+    return out, seg.value
+
+
+def render_cuda_compat(spheres, materials, camera, params, threads=None):
+    """The reference CUDA variant's semantics (src/CUDA/cuda_impl.cu): f32 (rows, width, 3)."""
+    spheres = np.ascontiguousarray(spheres, dtype=abi.SPHERE_DTYPE)
+    materials = np.ascontiguousarray(materials, dtype=abi.MATERIAL_DTYPE)
+    rows = params.height if params.flags & abi.RT_FLAG_FULL_FRAME else abi.rows_of(params)
+    out = np.zeros((rows, params.width, 3), dtype=np.float32)
+    seg = C.c_uint64(0)
+    threads = threads or min(8, os.cpu_count() or 1)
+    rc = lib().oracle_render_cuda_compat(abi.ptr(spheres, C.POINTER(abi.RtSphere)), len(spheres),
+                                         abi.ptr(materials, C.POINTER(abi.RtMaterial)), len(materials),
+                                         C.byref(camera), C.byref(params), threads,
+                                         abi.ptr(out, C.POINTER(C.c_float)), C.byref(seg))
     assert rc == 0, rc
     return out, seg.value
 

@@ -123,3 +123,40 @@ def test_save_ppm(tmp_path):
     rt.save_ppm(str(p), img)
     raw = p.read_bytes()
     assert raw.startswith(b"P6\n3 2\n255\n") and raw[len(b"P6\n3 2\n255\n"):] == img.tobytes()
+
+
+# ---- the reference's CUDA variant (RT_FLAG_CUDA_COMPAT; src/CUDA/cuda_impl.cu) -------------
+def test_cuda_variant_scene_and_camera():
+    """rt_scene_cuda / rt_camera_cuda: cuda_impl.cu:425-437 and :371-375, the camera basis bit
+    for bit as the oracle's camera ctor computes it for those arguments."""
+    s, m = rt.cuda_scene_arrays()
+    assert s["center"].tolist() == [[0, 0, -1], [0, -100.5, -1], [1, 0, -1], [-1, 0, -1], [-1, 0, -1]]
+    assert s["radius"].tolist() == [np.float32(v) for v in (.5, 100., .5, .5, -.499)]
+    assert s["material"].tolist() == [0, 3, 1, 2, 2]
+    assert m["kind"].tolist() == [abi.RT_LAMBERT, abi.RT_METAL, abi.RT_DIELECTRIC, abi.RT_LAMBERT]
+    assert m["param"].tolist() == [0, 0, 1.5, 0]
+    cam = rt.Camera.cuda(1280, 720)
+    f3 = C.c_float * 3
+    want = abi.RtCamera()
+    assert O.lib().oracle_camera_init(f3(0, 0, 0), f3(0, 0, -1), f3(0, 1, 0), np.float32(1280 / 720), 88.0, .0625,
+                                      1.0, 0, C.byref(want)) == 0
+    assert bytes(cam.c) == bytes(want)
+
+
+def test_cuda_variant_oracle_engine_and_pixel_zero():
+    """The restated xorshift32 engine (cuda_impl.cu:21-28) against the published sequence for
+    state 1 (Marsaglia 2003: 270369, 67634689, 2647435461); and pixel 0 with seed 0, whose
+    engine is the fixed point 0, renders (the default camera sends its rays to the sky)."""
+    x, seq = 1, []
+    for _ in range(3):
+        x ^= (x << 13) & 0xffffffff
+        x ^= x >> 17
+        x ^= (x << 5) & 0xffffffff
+        seq.append(x)
+    assert seq == [270369, 67634689, 2647435461]
+    s, m = rt.cuda_scene_arrays()
+    W, H = 8, 6
+    p = rt.make_params(W, H, 4, 32, 0, cuda_compat=True)
+    img, seg = O.render_cuda_compat(s, m, rt.Camera.cuda(W, H).c, p)
+    assert np.isfinite(img).all() and seg >= W * H * 4
+    assert (img[0, 0] > 0).all()  # sky colour

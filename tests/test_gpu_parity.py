@@ -310,3 +310,39 @@ def test_frames_in_flight_match_serial(monkeypatch):
         _bits_equal(outs[i].cpu().numpy(), want)
         assert int(segs[i][0]) == want_seg
     ds.close()
+
+
+# ---- the reference's CUDA variant (RT_FLAG_CUDA_COMPAT) ------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene_name,W,H,spp,depth,seed,rows", [
+    ("cuda", 64, 36, 48, 32, 0, None), ("cuda", 50, 31, 7, 32, 5, None), ("cuda", 64, 36, 16, 3, 0, (1, 2)),
+    ("cuda", 40, 30, 8, 0, 0, None), ("huge", 48, 32, 4, 32, 9, None), ("simple", 48, 27, 6, 64, 0, (0, 3))])
+def test_cuda_compat_matches_oracle(scene_name, W, H, spp, depth, seed, rows):
+    """compat_kernel (one lane per pixel, its xorshift32 engine sequential over the pixel's
+    samples) against the CPU restatement of src/CUDA/cuda_impl.cu: bit-identical f32 frames
+    and the same segment count, on the variant's scene and camera and on the CPU path's
+    scenes, with row partitions. Parity with the variant itself is unpinned (no nvcc here)."""
+    if scene_name == "cuda":
+        s, m = rt.cuda_scene_arrays()
+    else:
+        s, m = G.scene(scene_name)
+    kw = {} if rows is None else {"row_offset": rows[0], "row_stride": rows[1]}
+    p = rt.make_params(W, H, spp, depth, seed, cuda_compat=True, **kw)
+    cam = rt.Camera.cuda(W, H)
+    got, st = rt.render_f32((s, m), p, cam)
+    want, seg = O.render_cuda_compat(s, m, cam.c, p)
+    _bits_equal(got, want)
+    assert st.segments == seg
+
+
+@pytest.mark.gpu
+def test_cuda_impl_replacement_u8():
+    """rt_render_cuda_impl(W, H, out) = cuda_impl(W, H, image_texels): the variant's scene,
+    camera, 48 spp, 32 bounces, gamma 1/2.2 and (uint8)(255 c); +-1 LSB against the oracle's
+    f32 frame through the CPU epilogue (powf rounding)."""
+    W, H = 96, 54
+    got = rt.render_cuda_impl(W, H)
+    s, m = rt.cuda_scene_arrays()
+    want, _ = O.render_cuda_compat(s, m, rt.Camera.cuda(W, H).c, rt.make_params(W, H, 48, 32, 0, cuda_compat=True))
+    ref8 = O.epilogue_rgb8(want)
+    assert np.abs(got.astype(int) - ref8.astype(int)).max() <= 1

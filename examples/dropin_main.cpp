@@ -4,9 +4,11 @@
 // raytracer::data so the example builds without the reference; in the reference tree the real
 // types are used unchanged.
 //   g++ -std=c++20 -Iinclude examples/dropin_main.cpp -Lraytracinginoneweekend_amd -lrt_mi355x
-//       -Wl,-rpath,$PWD/raytracinginoneweekend_amd -o dropin && ./dropin out.ppm
+//       -Wl,-rpath,$PWD/raytracinginoneweekend_amd -o dropin && ./dropin out.ppm [spp | cuda]
+// With "cuda" it calls rt::cuda_impl, the CUDA variant's own scene and semantics.
 #include <cstdio>
 #include <fstream>
+#include <string>
 #include <variant>
 #include <vector>
 
@@ -37,9 +39,13 @@ int main(int argc, char **argv)
     d.spheres.push_back({{-2, 1, 0}, -.99f, 2});
     std::vector<ex::u8vec3> texels;
     try {
-        rt::settings s;
-        s.spp = argc > 2 ? static_cast<std::uint32_t>(std::atoi(argv[2])) : 16u;
-        rt::render_impl(d, W, H, texels, s);
+        if (argc > 2 && std::string(argv[2]) == "cuda") {
+            rt::cuda_impl(W, H, texels);  // was: cuda_impl(app_data.width, app_data.height, output)
+        } else {
+            rt::settings s;
+            s.spp = argc > 2 ? static_cast<std::uint32_t>(std::atoi(argv[2])) : 16u;
+            rt::render_impl(d, W, H, texels, s);
+        }
     } catch (const std::exception &e) {
         std::fprintf(stderr, "render failed: %s\n", e.what());
         return 3;

@@ -105,4 +105,17 @@ void render_impl(std::uint32_t width, std::uint32_t height, std::vector<Texel> &
     render_rgb8(spheres, materials, cam, width, height, s, image_texels);
 }
 
+// The CUDA variant itself, src/CUDA/cuda_impl.cu:384-453, under its own name and shape: its
+// scene (:425-437), camera (:371-375), 48 spp, 32 bounces, one xorshift32 engine per pixel
+// (RT_FLAG_CUDA_COMPAT). In the reference tree:
+//     void cuda_impl(std::uint32_t w, std::uint32_t h, std::vector<math::u8vec3> &t) { rt::cuda_impl(w, h, t); }
+template <class Texel>
+void cuda_impl(std::uint32_t width, std::uint32_t height, std::vector<Texel> &image_texels)
+{
+    static_assert(sizeof(Texel) == 3, "Texel must be a packed 3 x uint8 RGB type (math::u8vec3)");
+    image_texels.resize(static_cast<std::size_t>(width) * height);
+    check(rt_render_cuda_impl(width, height, reinterpret_cast<std::uint8_t *>(image_texels.data())),
+          "rt_render_cuda_impl");
+}
+
 } // namespace rt

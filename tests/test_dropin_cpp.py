@@ -43,3 +43,17 @@ def test_dropin_matches_python_binding(tmp_path):
     import raytracinginoneweekend_amd as rt
     ref, _ = rt.render_rgb8(rt.simple_scene_arrays(), rt.make_params(200, 100, 4, 64, 1234))
     np.testing.assert_array_equal(img, ref)
+
+
+@pytest.mark.gpu
+def test_dropin_cuda_impl_matches_python_binding(tmp_path):
+    """rt::cuda_impl (the CUDA variant's own shape and semantics) from C++ = rt.render_cuda_impl."""
+    exe = _build(tmp_path)
+    out = tmp_path / "c.ppm"
+    subprocess.run([exe, str(out), "cuda"], check=True)
+    raw = out.read_bytes()
+    hdr = b"P6\n200 100\n255\n"
+    assert raw.startswith(hdr)
+    img = np.frombuffer(raw[len(hdr):], dtype=np.uint8).reshape(100, 200, 3)
+    import raytracinginoneweekend_amd as rt
+    np.testing.assert_array_equal(img, rt.render_cuda_impl(200, 100))

@@ -14,11 +14,11 @@
  * buffers. The literal `cuda_impl`-shaped C++ drop-in lives in rt_render_impl.hpp.
  *
  * Semantics follow the reference CPU render path (src/main.cxx:120-215 with
- * src/raytracer.hxx, src/camera.hxx, src/math.hxx), not the CUDA variant (whose
- * different scene/sky/sampling is out of scope).
+ * src/raytracer.hxx, src/camera.hxx, src/math.hxx); the CUDA variant's own semantics
+ * (src/CUDA/cuda_impl.cu) are selected with RT_FLAG_CUDA_COMPAT or rt_render_cuda_impl.
  *
- * Threading: every call is synchronous unless its name ends in _async/_device; one
- * in-flight render per device. Errors: a negative status; rt_last_error() returns a
+ * Threading: every call is synchronous unless its name ends in _device; calls on one
+ * rt_scene come from one host thread. Errors: a negative status; rt_last_error() returns a
  * thread-local message for the last failing call on this thread.
  */
 #ifndef RT_API_H
@@ -179,13 +179,16 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres,
                     const rt_material *materials, uint32_t n_materials, int device,
                     rt_scene **out);
 int rt_scene_destroy(rt_scene *scene);
-/* Enqueue one render on `stream` (a hipStream_t, or NULL for the null stream).
+/* Enqueue one render for `stream` (a hipStream_t, or NULL for the null stream).
  * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64[3]
  * that accumulates {segments, sphere tests, cluster box tests} (zero it first). No
- * host sync.                                                                          */
+ * host sync. The render kernels run on one of two internal streams of the scene (double-
+ * buffered workspace) so consecutive frames overlap; they read only the scene and the
+ * by-value arguments, and the writes to d_rgb / d_segments are enqueued on `stream`, so
+ * results appear in stream order (RT_PIPELINE=0 in the environment: all on `stream`).   */
 int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
                      float *d_rgb, void *stream, uint64_t *d_segments);
-/* Durations (ms, HIP events on the render stream) of the render kernel launches of the
+/* Durations (ms, HIP events on the render kernels' stream) of the render kernel launches of the
  * most recent calls of rt_render_device on this scene, oldest first: entry i is the sum
  * over the passes of one call. Writes up to `max` entries, *n = entries written. Waits for
  * those calls to finish.                                                                */
@@ -195,12 +198,13 @@ int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n)
  * [1] wave refill rounds, [2] wave / [3] lane sphere blocks with a positive discriminant,
  * [4] wave / [5] lane root evaluations, [6] segments, [7] wave-level blocks of 8 cluster
  * members executed, [8..12] shader-clock cycles summed over waves per loop region
- * (refill, sample start, closest hit, shading, fold). Copies them out; reset zeroes.  */
+ * (refill, sample start + rejection loop, closest hit, shading, fold), [14] ~(earliest wave
+ * start, 100 MHz clock). Copies them out; reset zeroes.                                */
 int rt_scene_debug_counters(rt_scene *scene, uint64_t out[16], int reset);
 /* Diagnostics: per-wave records of the last instrumented render launch, out[4w .. 4w+3] for
- * wave w of the grid = {start, exit} (100 MHz realtime clock), loop iterations, and
- * (hardware CU id << 32 | refill rounds); at most max_waves records, *n = records written
- * (0 without RT_DEBUG_STATS=1).                                                          */
+ * wave w of the grid = {time the wave found every queue dry, exit} (100 MHz realtime
+ * clock), loop iterations, and (hardware CU id << 32 | iterations after dry << 16 | refill
+ * rounds); at most max_waves records, *n = records written (0 without RT_DEBUG_STATS=1).  */
 int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, uint32_t *n);
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,

@@ -290,6 +290,13 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
     Hit h{RT_TMAX, 0xffffffffu};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, a, h, dbg);
+#ifdef RT_DUP_ALWAYS  // timing-only build: the always-tested list twice
+    {
+        f3 o2 = o;
+        asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+        run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o2, d, a, h, dbg);
+    }
+#endif
     tests += p.n_always;
     if (CULL) {
         auto safe_rcp = [](float x) {
@@ -345,6 +352,13 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
                         const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
                         if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
                         run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
+#ifdef RT_DUP_MEMBERS  // timing-only build: each passing cluster's members twice
+                        {
+                            f3 o2 = o;
+                            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+                            run_members<FAST, STATS>(geo, sidx, start, cnt, o2, d, a, h, dbg);
+                        }
+#endif
                         tests += cnt << 16;
                     }
                     if (pb) {
@@ -352,6 +366,13 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
                         const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
                         if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
                         run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
+#ifdef RT_DUP_MEMBERS  // timing-only build: each passing cluster's members twice
+                        {
+                            f3 o2 = o;
+                            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+                            run_members<FAST, STATS>(geo, sidx, start, cnt, o2, d, a, h, dbg);
+                        }
+#endif
                         tests += cnt << 16;
                     }
                 }
@@ -667,6 +688,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         if (fresh || pend) {
             const uint64_t inc = fresh ? (((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo) : inc_data;
             uint64_t st = fresh ? rc : rng;
+#ifdef RT_DUP_REJECT  // timing-only build: the rejection loop twice (the copy is discarded)
+            {
+                uint64_t st2 = st;
+                asm volatile("" : "+v"(st2));
+                const f3 r2 = random_in_unit_sphere(st2, inc);
+                float sink = r2.x + r2.y + r2.z;
+                asm volatile("" ::"v"(sink));
+            }
+#endif
             const f3 r = random_in_unit_sphere(st, inc);
             if (fresh) {
                 // camera.hxx:46-57
@@ -712,6 +742,16 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         uint64_t cmask[2] = {0, 0};
         uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
         if (seg) h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, cmask);
+#ifdef RT_DUP_HIT  // timing-only build: the closest-hit search twice on an opaque copy of the ray
+        if (seg) {
+            f3 o2 = o;
+            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+            uint32_t t2 = 0;
+            uint64_t cm2[2] = {0, 0};
+            const Hit h2 = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o2, d, dbg, t2, cm2);
+            if (h2.t < h.t) h = h2;
+        }
+#endif
         if constexpr (CULL == 6) members_compacted<FAST, STATS>(geo, sidx, clus, wkey, wlist, cmask, o, d, h, dbg, tally);
         stamp(2);
         {

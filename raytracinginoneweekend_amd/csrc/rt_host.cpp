@@ -105,6 +105,7 @@ struct rt_scene {
     float clus_pad[2] = {0.f, 0.f};
     uint32_t n_clusters_real[2] = {0, 0}, n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     uint32_t shade_offset[2] = {0, 0};
+    uint32_t cluster_units = 2;  // blocks of 8 in the largest cluster
     // workspace, double-buffered for two frames in flight: render i runs on internal stream
     // xs[i % 2] into slots[i % 2] while the caller stream still accumulates frame i - 1
     float *slots[2] = {nullptr, nullptr};
@@ -282,10 +283,18 @@ struct blob_t {
 };
 
 constexpr float kPadRel = 1e-3f;      // must match RT_PAD_REL in rt_kernel.hip
-constexpr uint32_t kClusterMax = 16;  // spheres per cluster (two blocks of 8)
+// Spheres per cluster: 16 (two blocks of 8); RT_CLUSTER_SIZE (4..64, multiple of 4) for A/B,
+// read when a scene is created.
+uint32_t cluster_max()
+{
+    const char *e = std::getenv("RT_CLUSTER_SIZE");
+    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 16ul;
+    return v >= 4 && v <= 64 && v % 4 == 0 ? static_cast<uint32_t>(v) : 16u;
+}
 
 void split_clusters(const rt_sphere *s, std::vector<uint32_t> ids, std::vector<std::vector<uint32_t>> &out)
 {
+    const uint32_t kClusterMax = cluster_max();
     if (ids.size() <= kClusterMax) {
         out.push_back(std::move(ids));
         return;
@@ -316,7 +325,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     // every segment; big (> 4x) and small are clustered separately so that one big sphere
     // does not inflate the boxes of the small ones
     std::vector<uint32_t> always, big, small;
-    if (clustered && n >= 2 * kClusterMax) {
+    if (clustered && n >= 2 * cluster_max()) {
         std::vector<float> r(n);
         for (uint32_t i = 0; i < n; ++i) r[i] = std::fabs(s[i].radius);
         std::vector<float> sorted = r;
@@ -710,6 +719,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         sc->supers_offset[b] = blobs[b].supers_offset;
         sc->shade_offset[b] = blobs[b].shade_offset;
     }
+    sc->cluster_units = (cluster_max() + 7u) / 8u;
     if (rc == RT_OK) {
         hipError_t e = hipMalloc((void **)&sc->queue_ctr, kCtrWords * sizeof(uint32_t));
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -806,7 +816,10 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         k.dbg = sc->dbg;
     }
     const int b = cull ? 1 : 0;
-    const int cull_mode = cull ? cull_structure() : 0;
+    // structures 2 and 6 keep per-lane cluster masks of RT_MAX_CLUSTERS (128) bits; a scene
+    // with more clusters runs structure 5 (any count)
+    int cull_mode = cull ? cull_structure() : 0;
+    if ((cull_mode == 2 || cull_mode == 6) && sc->n_clusters[1] > 128) cull_mode = 5;
     k.blob = reinterpret_cast<const float4 *>(sc->blob[b]);
     k.blob_units = sc->blob_units[b];
     k.n_geo = sc->n_geo[b];
@@ -818,6 +831,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.n_supers = sc->n_supers[b];
     k.supers_offset = sc->supers_offset[b];
     k.use_root = root_box_env();
+    k.cluster_units = sc->cluster_units;
     k.shade_offset = sc->shade_offset[b];
     // the shading records (the blob's tail) join the geometry in LDS unless that costs
     // workgroups per CU; RT_SHADE_LDS=0/1 forces the choice for A/B

@@ -461,7 +461,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
 }
 
 // Structure 6, phase B: the member tests of every (lane, passing cluster) pair of the wave,
-// compacted. A pair is split into two units of 8 member slots (a cluster holds <= 16); the
+// compacted. A pair is split into units of 8 member slots (cluster_units per cluster); the
 // units are numbered by an exclusive prefix over the lanes (bit-plane ballots), dealt 64 per
 // round to ALL lanes of the wave (idle lanes included), and each unit's best candidate is
 // folded into its owner's LDS key with one ds_min_u64: key = bits(t) << 32 | original index,
@@ -473,7 +473,7 @@ template <bool FAST, bool STATS>
 __device__ __forceinline__ void members_compacted(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
                                                   const float4 *__restrict__ clus, uint64_t *wkey, uint32_t *wlist,
                                                   const uint64_t (&cmask)[2], f3 o, f3 d, Hit &h, Dbg &dbg,
-                                                  uint32_t &tests)
+                                                  uint32_t &tests, uint32_t p_units)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t k = (uint32_t)(__popcll(cmask[0]) + __popcll(cmask[1]));  // passing clusters
@@ -488,7 +488,8 @@ __device__ __forceinline__ void members_compacted(const float4 *__restrict__ geo
     T = __builtin_amdgcn_readfirstlane(T);
     if (T == 0) return;
     if (k) wkey[lane] = ((uint64_t)__float_as_uint(h.t) << 32) | h.id;
-    const uint32_t units = 2u * T;
+    const uint32_t U = p_units;  // blocks of 8 per cluster (cluster size / 8, rounded up)
+    const uint32_t units = U * T;
     for (uint32_t base = 0; base < units; base += 64u) {
         // emission: each owner writes its units in [base, base + 64)
         if (k) {
@@ -499,11 +500,11 @@ __device__ __forceinline__ void members_compacted(const float4 *__restrict__ geo
                 while (m) {
                     const uint32_t c = (uint32_t)__builtin_ctzll(m) + 64u * (uint32_t)w;
                     m &= m - 1u;
-                    const uint32_t u0 = 2u * (E + j++);
-                    if (u0 + 1u >= base && u0 < base + 64u) {
+                    const uint32_t u0 = U * (E + j++);
+                    if (u0 + U > base && u0 < base + 64u) {
                         const uint32_t e = lane | (c << 6);
-                        if (u0 >= base) wlist[u0 - base] = e;
-                        if (u0 + 1u < base + 64u) wlist[u0 + 1u - base] = e | (1u << 13);
+                        for (uint32_t hb = 0; hb < U; ++hb)
+                            if (u0 + hb >= base && u0 + hb < base + 64u) wlist[u0 + hb - base] = e | (hb << 13);
                     }
                 }
             }
@@ -518,7 +519,7 @@ __device__ __forceinline__ void members_compacted(const float4 *__restrict__ geo
         const f3 ro = mk(__shfl(o.x, owner), __shfl(o.y, owner), __shfl(o.z, owner));
         const f3 rd = mk(__shfl(d.x, owner), __shfl(d.y, owner), __shfl(d.z, owner));
         if (lane < n_here) {
-            const uint32_t c = (e >> 6) & 127u, half = e >> 13;
+            const uint32_t c = (e >> 6) & 127u, half = e >> 13;  // half: the unit's block of 8
             const uint32_t sc = __float_as_uint(clus[2 * c + 1].w);
             const uint32_t start = sc & 0xffffu, cnt = sc >> 16;
             if (8u * half < cnt) {
@@ -752,7 +753,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             if (h2.t < h.t) h = h2;
         }
 #endif
-        if constexpr (CULL == 6) members_compacted<FAST, STATS>(geo, sidx, clus, wkey, wlist, cmask, o, d, h, dbg, tally);
+        if constexpr (CULL == 6)
+            members_compacted<FAST, STATS>(geo, sidx, clus, wkey, wlist, cmask, o, d, h, dbg, tally, p.cluster_units);
         stamp(2);
         {
             const uint32_t al = seg ? p.n_always : 0u;

@@ -346,3 +346,40 @@ def test_cuda_impl_replacement_u8():
     want, _ = O.render_cuda_compat(s, m, rt.Camera.cuda(W, H).c, rt.make_params(W, H, 48, 32, 0, cuda_compat=True))
     ref8 = O.epilogue_rgb8(want)
     assert np.abs(got.astype(int) - ref8.astype(int)).max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cluster_size", ["4", "8", "12", "24", "32", "64"])
+@pytest.mark.parametrize("structure", ["5", "6"])
+def test_cluster_size_bit_exact(cluster_size, structure, monkeypatch):
+    """Any cluster size (RT_CLUSTER_SIZE, read when the scene is created) and loop structure
+    gives the oracle's bits: structure 6 deals ceil(size / 8) units of 8 members per
+    (lane, cluster) pair."""
+    monkeypatch.setenv("RT_CLUSTER_SIZE", cluster_size)
+    monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
+    rng = np.random.default_rng(11)
+    for s, m in (G.scene("huge"), _random_scene(rng, 900, 10.0)):
+        W, H, spp = 40, 24, 4
+        cam = O.camera_default(W, H, abi.RT_CAMERA_CORRECTED)
+        p = rt.make_params(W, H, spp, 64, 3)
+        got, st = rt.render_f32((s, m), p, cam)
+        want, seg = O.render_f32(s, m, cam, p)
+        _bits_equal(got, want)
+        assert st.segments == seg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("structure", ["2", "5", "6"])
+def test_many_clusters_bit_exact(structure, monkeypatch):
+    """A scene with more than 128 clusters (5000 spheres): structures 2 and 6, whose per-lane
+    masks hold 128 clusters, fall back to structure 5; every structure gives the oracle's bits."""
+    monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
+    rng = np.random.default_rng(5)
+    s, m = _random_scene(rng, 5000, 40.0)
+    W, H, spp = 32, 24, 2
+    cam = O.camera_default(W, H, abi.RT_CAMERA_CORRECTED)
+    p = rt.make_params(W, H, spp, 64, 1)
+    got, st = rt.render_f32((s, m), p, cam)
+    want, seg = O.render_f32(s, m, cam, p)
+    _bits_equal(got, want)
+    assert st.segments == seg

@@ -106,8 +106,9 @@ struct rt_scene {
     uint32_t n_clusters_real[2] = {0, 0}, n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     uint32_t shade_offset[2] = {0, 0};
     uint32_t cluster_units = 2;  // blocks of 8 in the largest cluster
-    // workspace, double-buffered for two frames in flight: render i runs on internal stream
-    // xs[i % 2] into slots[i % 2] while the caller stream still accumulates frame i - 1
+    // workspace, double-buffered: consecutive render passes (of one frame or of consecutive
+    // frames) alternate between internal streams xs[b] and workspaces slots[b], so a pass renders
+    // while the caller stream still accumulates the previous one
     float *slots[2] = {nullptr, nullptr};
     size_t slots_bytes[2] = {0, 0};
     float *acc = nullptr;
@@ -115,7 +116,8 @@ struct rt_scene {
     uint32_t *queue_ctr = nullptr;  // [2][8 queues x kQueueStride], then [2][3] u64 segment counters
     hipStream_t xs[2] = {nullptr, nullptr};
     hipEvent_t ev_done[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
-    bool free_valid[2] = {false, false};  // 8 queue counters, one 256-B line each
+    bool free_valid[2] = {false, false};
+    uint32_t next_buf = 0;  // workspace of the next render pass  // 8 queue counters, one 256-B line each
     int cu_count = 0;
     int occ[4][7][2];  // [variant][cull structure 0-6][shade records in LDS] blocks per CU, -1 = not queried
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
@@ -864,31 +866,35 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     if (spp_pass == 0) spp_pass = 4;
     if (n_pixels * std::min<uint64_t>(spp_pass, P.spp) >= (1ull << 31) - 8192)
         return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
-    // frames in flight: the render kernels of this call run on internal stream xs[b] with
-    // workspace b, ordered only after the caller-stream work that last read workspace b (the
-    // accumulation of call i - 2); they touch no caller memory, so the caller stream sees the
-    // same results in the same order. RT_PIPELINE=0: everything on the caller stream.
-    const uint32_t wb = static_cast<uint32_t>(sc->calls & 1u);
+    // frames in flight: each render pass runs on internal stream xs[b] with workspace b,
+    // ordered only after the caller-stream work that last read workspace b (the accumulation
+    // of the pass two before); render kernels touch no caller memory, so the caller stream sees
+    // the same results in the same order. RT_PIPELINE=0: everything on the caller stream.
     const bool pipe = pipeline_env();
-    hipStream_t xst = pipe ? sc->xs[wb] : st;
-    if (int rc = ensure((void **)&sc->slots[wb], &sc->slots_bytes[wb], per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc)
-        return rc;
     if (spp_pass < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
-    k.slots = sc->slots[wb];
+    for (int w = 0; w < (pipe ? 2 : 1); ++w)
+        if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc)
+            return rc;
     k.chunk_items = chunk_items();
-    k.queue_ctr = sc->queue_ctr + wb * 8u * rt::kQueueStride;
-    unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + 16u * rt::kQueueStride) + 4u * wb;
-    k.segments = d_segments ? (pipe ? seg_b : reinterpret_cast<unsigned long long *>(d_segments)) : nullptr;
-    if (pipe && sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(xst, sc->ev_free[wb], 0));
-    if (pipe && d_segments) RT_HIP(hipMemsetAsync(seg_b, 0, 3 * sizeof(unsigned long long), xst));
 
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
-    RT_HIP(hipEventRecord(sc->ev_begin[ring], xst));
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     for (uint32_t s0 = 0; s0 < P.spp; s0 += static_cast<uint32_t>(spp_pass)) {
         const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
+        // every pass takes the other workspace (and stream): pass p + 1's render overlaps pass
+        // p's drain and accumulation, within a frame and across frames
+        const uint32_t wb = pipe ? sc->next_buf : 0u;
+        sc->next_buf ^= 1u;
+        hipStream_t xst = pipe ? sc->xs[wb] : st;
+        k.slots = sc->slots[wb];
+        k.queue_ctr = sc->queue_ctr + wb * 8u * rt::kQueueStride;
+        unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + 16u * rt::kQueueStride) + 4u * wb;
+        k.segments = d_segments ? (pipe ? seg_b : reinterpret_cast<unsigned long long *>(d_segments)) : nullptr;
+        if (pipe && sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(xst, sc->ev_free[wb], 0));
+        if (pipe && d_segments) RT_HIP(hipMemsetAsync(seg_b, 0, 3 * sizeof(unsigned long long), xst));
+        if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], xst));
         k.sample_begin = s0;
         k.sample_end = s1;
         fill_frame_consts(k);
@@ -901,7 +907,6 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         }
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_items + 255u) / 256u)));
-        if (pipe && s0 > 0) RT_HIP(hipStreamWaitEvent(xst, sc->ev_free[wb], 0));  // previous pass accumulated
         RT_HIP(hipMemsetAsync(k.queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), xst));
         if (verbose())
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) chunk=%u\n",
@@ -930,7 +935,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         a.row_offset = k.row_offset;
         a.row_stride = k.row_stride;
         a.full_frame = k.full_frame;
-        if (pipe && s1 == P.spp && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
+        if (pipe && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
         RT_HIP(rt::launch_accumulate(a, st));
         if (pipe) {
             RT_HIP(hipEventRecord(sc->ev_free[wb], st));

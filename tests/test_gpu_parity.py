@@ -286,11 +286,15 @@ def test_chunking_and_passes_bit_exact(chunk, budget_samples, shade_lds, monkeyp
 
 
 @pytest.mark.gpu
-def test_frames_in_flight_match_serial(monkeypatch):
-    """Consecutive rt_render_device calls on one scene overlap (render kernels on internal
-    streams, double-buffered workspaces); every frame must still equal its serial render,
-    with different cameras, spp and row partitions back to back and no sync between calls."""
+@pytest.mark.parametrize("budget_samples", [0, 4])
+def test_frames_in_flight_match_serial(budget_samples, monkeypatch):
+    """Consecutive rt_render_device calls on one scene overlap (render passes on internal
+    streams, double-buffered workspaces, alternating per pass); every frame must still equal
+    its serial render, with different cameras, spp and row partitions back to back and no sync
+    between calls, in one pass per frame or in passes of 4 samples."""
     import torch
+    if budget_samples:
+        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(48 * 32 * 12 * budget_samples))
     s, m = G.scene("huge")
     W, H = 48, 32
     jobs = [(rt.make_params(W, H, 8, 64, 1), O.camera_default(W, H, abi.RT_CAMERA_REFERENCE), H),

@@ -25,7 +25,7 @@
 
 namespace rt {
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream);
-hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
+hipError_t occupancy_render(int variant, int cull, bool deep, int *blocks_per_cu, size_t lds);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream);
 hipError_t occupancy_compat(int *blocks_per_cu);
@@ -119,7 +119,7 @@ struct rt_scene {
     bool free_valid[2] = {false, false};
     uint32_t next_buf = 0;  // workspace of the next render pass  // 8 queue counters, one 256-B line each
     int cu_count = 0;
-    int occ[4][7][2];  // [variant][cull structure 0-6][shade records in LDS] blocks per CU, -1 = not queried
+    int occ[4][7][2][2];  // [variant][cull structure 0-6][deep wave][shade records in LDS] blocks per CU, -1 = unknown
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
@@ -573,6 +573,15 @@ bool pipeline_env()
     return !(e && e[0] == '0');
 }
 
+// Segments after which waves 0-2 hand a path to the workgroup's deep wave (RT_DEEP_DEPTH;
+// 0 = no deep wave).
+uint32_t deep_depth_env()
+{
+    const char *e = std::getenv("RT_DEEP_DEPTH");
+    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 0ul;
+    return v <= 255 ? static_cast<uint32_t>(v) : 0u;
+}
+
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
 bool debug_stats()
 {
@@ -698,7 +707,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         std::memcpy(b.data.data() + at, kinds.data(), kinds.size());
     }
     rt_scene *sc = new rt_scene();
-    for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
+    for (auto &r : sc->occ) for (auto &x : r) for (auto &y : x) y[0] = y[1] = -1;
     sc->device = device;
     sc->n_spheres = n_spheres;
     sc->n_materials = n_materials;
@@ -834,14 +843,16 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.supers_offset = sc->supers_offset[b];
     k.use_root = root_box_env();
     k.cluster_units = sc->cluster_units;
+    // deep-path wave: structures 0 and 5 (RT_DEEP_DEPTH, 0 = off)
+    k.deep_depth = (cull_mode == 0 || cull_mode == 5) && variant != rt::V_EXACT_SCALAR ? deep_depth_env() : 0u;
     k.shade_offset = sc->shade_offset[b];
     // the shading records (the blob's tail) join the geometry in LDS unless that costs
     // workgroups per CU; RT_SHADE_LDS=0/1 forces the choice for A/B
     auto occ_for = [&](int in_lds, int *out) -> int {
-        int &o = sc->occ[variant][cull_mode][in_lds];
+        int &o = sc->occ[variant][cull_mode][k.deep_depth != 0][in_lds];
         if (o < 0) {
             const size_t bytes = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(in_lds ? k.blob_units : k.shade_offset) * 16u;
-            RT_HIP(rt::occupancy_render(variant, cull_mode, &o, bytes));
+            RT_HIP(rt::occupancy_render(variant, cull_mode, k.deep_depth != 0, &o, bytes));
             o = std::max(o, 1);
         }
         *out = o;

@@ -546,7 +546,23 @@ __device__ __forceinline__ void members_compacted(const float4 *__restrict__ geo
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
 #endif
-template <int V, int CULL, bool STATS>
+// ---- deep paths: one wave per workgroup takes them over --------------------------------
+// 0.18% of config 3's samples never leave the glass sphere and run to max_depth; those and
+// other deep paths are 10% of the segments but, spread over every wave, make almost every
+// wave iteration pay for their dielectric shading and cluster members. With DEEP, waves 0-2 of
+// a workgroup park a path that is about to trace segment p.deep_depth + 1 in a workgroup LDS
+// queue (when it has room) and refill the lane; wave 3 takes parked paths before new items,
+// so deep paths share waves with each other. The result is unchanged: a path's state moves
+// whole, and every sample still lands in its own slot.
+constexpr uint32_t kDeepQ = 64;
+struct DeepQueue {
+    uint32_t head, tail, producers, pad;  // head: claimed by producers; tail: consumed by wave 3
+    uint32_t gen[kDeepQ];                 // slot generation (pos / kDeepQ + 1) once written
+    uint4 st[kDeepQ][5];                  // bits of o, d, att, {rng lo, rng hi, pix, ls}, pn
+    uint32_t meta[kDeepQ];                // depth | pend << 8 | pend_metal << 9
+};
+
+template <int V, int CULL, bool STATS, bool DEEP>
 __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(const KParams p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
@@ -554,13 +570,23 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     // [geo float4 x n_geo][sidx u32 x n_geo, 16-B padded][clusters float4 x 2 x n_clusters]
     extern __shared__ float4 lds_blob[];
     const float4 *blob;
+    DeepQueue *dq = nullptr;
+    if constexpr (DEEP) {
+        __shared__ DeepQueue s_dq;
+        dq = &s_dq;
+        if (threadIdx.x < kDeepQ) dq->gen[threadIdx.x] = 0u;
+        if (threadIdx.x == 0) { dq->head = 0u; dq->tail = 0u; dq->producers = 3u; }
+    }
     if constexpr (V == V_EXACT_SCALAR) {
         blob = p.blob;
+        if (DEEP) __syncthreads();
     } else {
         for (uint32_t i = threadIdx.x; i < p.lds_units; i += blockDim.x) lds_blob[i] = p.blob[i];
         __syncthreads();
         blob = lds_blob;
     }
+    const bool deep_wave = DEEP && (threadIdx.x >> 6) == 3u;  // the consumer of parked paths
+    uint32_t qtail = 0;                                        // deep wave: its copy of dq->tail
     // Per-render constants used only where a sample or an item starts are re-read from the
     // kernarg segment at each use (scalar loads) through a pointer made opaque every loop
     // iteration, so they do not pin ~30 SGPRs for the whole kernel (SGPR count bounds the
@@ -622,6 +648,40 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         // ---- refill items for idle lanes and start their samples -------------------
         uint64_t need = __ballot(!alive);
         bool fresh = false;
+        if (DEEP && deep_wave && need) {
+            // parked paths first, in queue order; a slot is read once its producer has
+            // published it (generation), and tail moves only after the reads
+            const uint32_t h = __builtin_amdgcn_readfirstlane(__atomic_load_n(&dq->head, __ATOMIC_ACQUIRE));
+            const uint32_t k = min((uint32_t)__popcll(need), h - qtail);
+            if (k) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                if (!alive && rank < k) {
+                    const uint32_t pos = qtail + rank, sl = pos % kDeepQ;
+                    while (__atomic_load_n(&dq->gen[sl], __ATOMIC_ACQUIRE) != pos / kDeepQ + 1u)
+                        __builtin_amdgcn_s_sleep(1);
+                    const uint4 a0 = dq->st[sl][0], a1 = dq->st[sl][1], a2 = dq->st[sl][2], a3 = dq->st[sl][3];
+                    const uint4 a4 = dq->st[sl][4];
+                    const uint32_t mt = dq->meta[sl];
+                    o = mk(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z));
+                    d = mk(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z));
+                    att = mk(__uint_as_float(a2.x), __uint_as_float(a2.y), __uint_as_float(a2.z));
+                    pn = make_float4(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z),
+                                     __uint_as_float(a4.w));
+                    rng = ((uint64_t)a3.y << 32) | a3.x;
+                    pix = a3.z;
+                    ls = a3.w;
+                    depth = mt & 0xffu;
+                    pend = (mt >> 8) & 1u;
+                    pend_metal = (mt >> 9) & 1u;
+                    alive = true;
+                }
+                qtail += k;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __atomic_store_n(&dq->tail, qtail, __ATOMIC_RELEASE);
+                need = __ballot(!alive);
+            }
+        }
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
             if (cnext >= cend) {
@@ -728,7 +788,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
             }
         }
         stamp(1);
-        if (__ballot(alive) == 0) break;  // only when the item space is exhausted
+        if (__ballot(alive) == 0) {  // only when the item space is exhausted
+            if (!DEEP || !deep_wave) break;
+            // the deep wave leaves once no producer is left and the queue is empty
+            const uint32_t h = __builtin_amdgcn_readfirstlane(__atomic_load_n(&dq->head, __ATOMIC_ACQUIRE));
+            const uint32_t pr = __builtin_amdgcn_readfirstlane(__atomic_load_n(&dq->producers, __ATOMIC_ACQUIRE));
+            if (pr == 0u && h == qtail) break;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
         if (STATS && lane == 0) {
             ++dbg_iters;
             if (exhausted) {
@@ -844,6 +912,47 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
                 dst[2] = col.z;
             }
         }
+        if constexpr (DEEP) {
+            // waves 0-2: park paths that reach p.deep_depth segments (room permitting)
+            const uint64_t pm = deep_wave ? 0ull : __ballot(alive && depth >= p.deep_depth);
+            if (pm) {
+                const uint32_t n = (uint32_t)__popcll(pm);
+                uint32_t h0 = 0, n2 = 0;
+                if (lane == __builtin_ctzll(pm)) {
+                    for (;;) {
+                        const uint32_t h = __atomic_load_n(&dq->head, __ATOMIC_RELAXED);
+                        const uint32_t t = __atomic_load_n(&dq->tail, __ATOMIC_ACQUIRE);
+                        n2 = min(n, kDeepQ - (h - t));
+                        h0 = h;
+                        if (n2 == 0u) break;
+                        uint32_t expect = h;
+                        if (__atomic_compare_exchange_n(&dq->head, &expect, h + n2, false, __ATOMIC_ACQ_REL,
+                                                        __ATOMIC_RELAXED))
+                            break;
+                    }
+                }
+                h0 = __builtin_amdgcn_readlane(h0, __builtin_ctzll(pm));
+                n2 = __builtin_amdgcn_readlane(n2, __builtin_ctzll(pm));
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+                if ((pm >> lane) & 1ull && rank < n2) {
+                    const uint32_t pos = h0 + rank, sl = pos % kDeepQ;
+                    dq->st[sl][0] = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), 0u);
+                    dq->st[sl][1] = make_uint4(__float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z), 0u);
+                    dq->st[sl][2] = make_uint4(__float_as_uint(att.x), __float_as_uint(att.y), __float_as_uint(att.z), 0u);
+                    dq->st[sl][3] = make_uint4((uint32_t)rng, (uint32_t)(rng >> 32), pix, ls);
+                    dq->st[sl][4] = make_uint4(__float_as_uint(pn.x), __float_as_uint(pn.y), __float_as_uint(pn.z),
+                                               __float_as_uint(pn.w));
+                    dq->meta[sl] = depth | ((uint32_t)pend << 8) | ((uint32_t)pend_metal << 9);
+                    __atomic_store_n(&dq->gen[sl], pos / kDeepQ + 1u, __ATOMIC_RELEASE);
+                    alive = false;
+                    pend = false;  // the pending scatter left with the path
+                }
+            }
+        }
+    }
+    if constexpr (DEEP) {
+        if (!deep_wave && lane == 0) __atomic_fetch_sub(&dq->producers, 1u, __ATOMIC_RELEASE);
     }
 
     if (p.segments) {
@@ -1125,40 +1234,44 @@ __global__ __launch_bounds__(256) void epilogue_rgb8_kernel(const float *in, uin
 }
 
 // ---- launchers (called from rt_host.cpp) ---------------------------------------------
-template <int V, bool STATS> static const void *ptr3(int cull)
+template <int V, bool STATS> static const void *ptr3(int cull, bool deep)
 {
-    if (cull == 1) return reinterpret_cast<const void *>(&render_kernel<V, 1, STATS>);
-    if (cull == 2) return reinterpret_cast<const void *>(&render_kernel<V, 2, STATS>);
-    if (cull == 3) return reinterpret_cast<const void *>(&render_kernel<V, 3, STATS>);
-    if (cull == 4) return reinterpret_cast<const void *>(&render_kernel<V, 4, STATS>);
-    if (cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS>);
-    if (cull == 6) return reinterpret_cast<const void *>(&render_kernel<V, 6, STATS>);
-    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS>);
+    if (deep && cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS, true>);
+    if (deep && cull == 0) return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, true>);
+    if (deep) return nullptr;
+    if (cull == 1) return reinterpret_cast<const void *>(&render_kernel<V, 1, STATS, false>);
+    if (cull == 2) return reinterpret_cast<const void *>(&render_kernel<V, 2, STATS, false>);
+    if (cull == 3) return reinterpret_cast<const void *>(&render_kernel<V, 3, STATS, false>);
+    if (cull == 4) return reinterpret_cast<const void *>(&render_kernel<V, 4, STATS, false>);
+    if (cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS, false>);
+    if (cull == 6) return reinterpret_cast<const void *>(&render_kernel<V, 6, STATS, false>);
+    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, false>);
 }
 
-static const void *render_ptr(int variant, int cull)
+static const void *render_ptr(int variant, int cull, bool deep)
 {
     switch (variant) {
-    case V_EXACT_LDS: return ptr3<V_EXACT_LDS, false>(cull);
-    case V_FAST_LDS: return ptr3<V_FAST_LDS, false>(cull);
-    case V_EXACT_SCALAR: return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false>);
-    case V_STATS_LDS: return ptr3<V_EXACT_LDS, true>(cull);
+    case V_EXACT_LDS: return ptr3<V_EXACT_LDS, false>(cull, deep);
+    case V_FAST_LDS: return ptr3<V_FAST_LDS, false>(cull, deep);
+    case V_EXACT_SCALAR:
+        return cull || deep ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false, false>);
+    case V_STATS_LDS: return ptr3<V_EXACT_LDS, true>(cull, deep);
     default: return nullptr;
     }
 }
 
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream)
 {
-    const void *fn = render_ptr(variant, cull);
+    const void *fn = render_ptr(variant, cull, p.deep_depth != 0);
     if (!fn) return hipErrorInvalidValue;
     const size_t lds = (size_t)p.lds_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};
     return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, stream);
 }
 
-hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds)
+hipError_t occupancy_render(int variant, int cull, bool deep, int *blocks_per_cu, size_t lds)
 {
-    const void *fn = render_ptr(variant, cull);
+    const void *fn = render_ptr(variant, cull, deep);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
 }

@@ -387,3 +387,25 @@ def test_many_clusters_bit_exact(structure, monkeypatch):
     want, seg = O.render_f32(s, m, cam, p)
     _bits_equal(got, want)
     assert st.segments == seg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deep,brute,budget_samples", [("1", False, 0), ("2", False, 0), ("2", True, 0),
+                                                        ("8", False, 0), ("2", False, 4), ("3", True, 8)])
+def test_deep_wave_bit_exact(deep, brute, budget_samples, monkeypatch):
+    """RT_DEEP_DEPTH: waves 0-2 of a workgroup hand paths that reach `deep` segments to wave 3
+    through an LDS queue (whole path state, pending scatter included); the oracle's bits and
+    segment count for the huge scene (glass-sphere paths run to max_depth) with culling or
+    brute force, in one pass or several."""
+    monkeypatch.setenv("RT_DEEP_DEPTH", deep)
+    if budget_samples:
+        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(96 * 40 * 12 * budget_samples))
+    s, m = G.scene("huge")
+    W, H, spp = 96, 40, 9
+    for mode in (abi.RT_CAMERA_REFERENCE, abi.RT_CAMERA_CORRECTED):
+        cam = O.camera_default(W, H, mode)
+        p = rt.make_params(W, H, spp, 64, 13, brute_force=brute)
+        got, st = rt.render_f32((s, m), p, cam)
+        want, seg = O.render_f32(s, m, cam, p)
+        _bits_equal(got, want)
+        assert st.segments == seg

@@ -86,6 +86,20 @@ __device__ __forceinline__ float canonical(uint64_t &st, uint64_t inc)
 __device__ __forceinline__ f3 random_in_unit_sphere(uint64_t &st, uint64_t inc)
 {
     f3 p;
+#ifdef RT_REJECT_FIXED  // timing-only build: exactly N attempts, first accepted kept (wrong bits)
+    bool got = false;
+    p = mk(0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < RT_REJECT_FIXED; ++k) {
+        float x = canonical(st, inc) * 2.f + -1.f;
+        float y = canonical(st, inc) * 2.f + -1.f;
+        float z = canonical(st, inc) * 2.f + -1.f;
+        const bool ok = !got && !(x * x + y * y + z * z > 0x1.000002p+0f);
+        p = ok ? mk(x, y, z) : p;
+        got = got || ok;
+    }
+    return p;
+#endif
     do {
         float x = canonical(st, inc) * 2.f + -1.f;
         float y = canonical(st, inc) * 2.f + -1.f;

@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=240, help="rows in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--rehearse-world", type=int, default=0,
+                    help="diagnostic, 1 GPU: render only rank 0's rows of an N-way split (no gather) to "
+                         "estimate one rank's frame time at N GPUs; not a bench line")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_render_c3.json"),
                     help="PMC summary of this kernel (scripts/pmc_round.sh) for roofline.traffic / VALU busy")
     return ap.parse_args()
@@ -83,6 +86,19 @@ def pmc_fields(path, kernel, config):
     if rec.get("kernel") != kernel or rec.get("config") != config:
         return None
     return rec
+
+
+def pass_spp(n_pixels, spp):
+    """Samples per render pass (rt_host.cpp: a 2 GiB slot workspace, multiples of 4)."""
+    per = (1 << 31) // (n_pixels * 12)
+    return spp if per >= spp else max(4, per & ~3)
+
+
+def frames_in_flight(pass_items):
+    """Render passes in flight (RT_PIPELINE, rt_host.cpp pipeline_env: by default 3 for passes
+    of at most 32 Mi samples, else 2; at most 4)."""
+    v = os.environ.get("RT_PIPELINE", "")
+    return (3 if pass_items <= 32 << 20 else 2) if not v else max(1, min(int(v), 4))
 
 
 def cpu_baseline(cfg, camera, seed, rows, threads):
@@ -153,7 +169,8 @@ def main():
     mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
     cam = rt.Camera.cuda(W, H) if compat else rt.Camera.default(W, H, mode)
     from raytracinginoneweekend_amd.rowtiles import FrameGather, rank_params
-    params = rank_params(W, H, spp, world, rank, max_depth=depth, seed=args.seed,
+    rehearse = args.rehearse_world if world == 1 and args.rehearse_world > 1 else 0
+    params = rank_params(W, H, spp, rehearse or world, rank, max_depth=depth, seed=args.seed,
                          scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast",
                          brute_force=args.traversal == "brute", cuda_compat=compat)
     rows = params.num_rows
@@ -166,7 +183,8 @@ def main():
 
     def step(count_segments):
         ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
-        gather(tile)
+        if not rehearse:
+            gather(tile)
 
     for _ in range(args.warmup):
         step(False)
@@ -210,7 +228,7 @@ def main():
     else:
         segments_all = segments
 
-    primaries = W * H * spp * args.steps
+    primaries = W * rows * spp * args.steps if rehearse else W * H * spp * args.steps
     value = primaries / elapsed / 1e6
     # roofline of the dominant kernel (render_kernel) on this rank
     k_avg_ms = sum(kt) / len(kt)
@@ -240,7 +258,7 @@ def main():
                        + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
             "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
             "frame_latency_ms": round(latency * 1e3, 3),
-            "frames_in_flight": 1 if os.environ.get("RT_PIPELINE") == "0" else 2,
+            "frames_in_flight": frames_in_flight(W * rows * pass_spp(W * rows, spp)),
             "segments_per_primary": round(segments_all / primaries, 4),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
@@ -263,7 +281,10 @@ def main():
             rec["roofline"]["traffic_unit"] = "bytes/launch"
             rec["roofline"]["valu_busy"] = pmc["valu_busy"]
             rec["roofline"]["pmc_source"] = os.path.relpath(args.pmc, REPO)
-        if world == 1 and not args.no_cpu_baseline:
+        if rehearse:
+            rec["rehearsal"] = (f"rank 0 of {rehearse}: rows 0, {rehearse}, ... ({rows} rows), no gather; value = "
+                                f"this rank's Mrays/s, x{rehearse} for the ideal {rehearse}-GPU job")
+        if world == 1 and not args.no_cpu_baseline and not rehearse:
             rec["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], args.camera, args.seed, args.cpu_rows,
                                                args.cpu_threads)
         print(json.dumps(rec), flush=True)

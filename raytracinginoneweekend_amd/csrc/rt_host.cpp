@@ -64,8 +64,13 @@ hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.
 
 constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 GiB)
 // 2 x 8 queue lines, 2 x 4 u64 segment counters, then the compat kernel's pixel counter
-constexpr size_t kCtrWords = 17 * rt::kQueueStride + 16;
-constexpr size_t kCompatCtr = 16 * rt::kQueueStride + 16;
+// workspaces for frames in flight (RT_PIPELINE = 2..kMaxBufs)
+constexpr uint32_t kMaxBufs = 4;
+// counters: [kMaxBufs][8 queues x kQueueStride], then [kMaxBufs][4] u64 segment counters, then
+// the compat kernel's counter
+constexpr size_t kSegWords = kMaxBufs * 8 * rt::kQueueStride;
+constexpr size_t kCompatCtr = kSegWords + kMaxBufs * 8 + 16;
+constexpr size_t kCtrWords = kCompatCtr + rt::kQueueStride;
 
 // RT_SLOT_BUDGET_BYTES lowers the per-pass slot workspace (tests force multi-pass renders).
 uint64_t slot_budget()
@@ -106,18 +111,18 @@ struct rt_scene {
     uint32_t n_clusters_real[2] = {0, 0}, n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     uint32_t shade_offset[2] = {0, 0};
     uint32_t cluster_units = 2;  // blocks of 8 in the largest cluster
-    // workspace, double-buffered: consecutive render passes (of one frame or of consecutive
-    // frames) alternate between internal streams xs[b] and workspaces slots[b], so a pass renders
-    // while the caller stream still accumulates the previous one
-    float *slots[2] = {nullptr, nullptr};
-    size_t slots_bytes[2] = {0, 0};
+    // workspaces: consecutive render passes (of one frame or of consecutive frames) rotate over
+    // internal streams xs[b] and workspaces slots[b], so a pass renders while the caller stream
+    // still accumulates the previous ones
+    float *slots[kMaxBufs] = {};
+    size_t slots_bytes[kMaxBufs] = {};
     float *acc = nullptr;
     size_t acc_bytes = 0;
-    uint32_t *queue_ctr = nullptr;  // [2][8 queues x kQueueStride], then [2][3] u64 segment counters
-    hipStream_t xs[2] = {nullptr, nullptr};
-    hipEvent_t ev_done[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
-    bool free_valid[2] = {false, false};
-    uint32_t next_buf = 0;  // workspace of the next render pass  // 8 queue counters, one 256-B line each
+    uint32_t *queue_ctr = nullptr;  // kCtrWords: queue and segment counters (layout at kCtrWords)
+    hipStream_t xs[kMaxBufs] = {};
+    hipEvent_t ev_done[kMaxBufs] = {}, ev_free[kMaxBufs] = {};
+    bool free_valid[kMaxBufs] = {};
+    uint32_t next_buf = 0;  // workspace of the next render pass
     int cu_count = 0;
     int occ[4][7][2][2];  // [variant][cull structure 0-6][deep wave][shade records in LDS] blocks per CU, -1 = unknown
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
@@ -566,11 +571,20 @@ namespace {
 int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, float *d_rgb, hipStream_t st,
                   uint64_t *d_segments);
 
-// RT_PIPELINE=0 runs the render kernels on the caller stream (no frames in flight).
-bool pipeline_env()
+// Render passes in flight: RT_PIPELINE=0 (or 1) runs the render kernels on the caller stream;
+// 2..kMaxBufs rotate that many internal streams and workspaces. Default: 3 for passes of at
+// most kShortPassItems samples, whose launch is short next to its drain (the max-depth paths
+// take the same ~64 iterations whatever the pass size; measured on an 8-way row share of
+// config 3, 14.7 M samples: 0.77 ms/frame with 3 vs 0.84 with 2), else 2 (no gain measured on
+// full frames, and each render's own duration stays close to a launch alone). 4 is not faster:
+// with the caller's stream that is more streams than the process's 4 hardware queues.
+constexpr uint64_t kShortPassItems = 32ull << 20;
+uint32_t pipeline_env(uint64_t pass_items)
 {
     const char *e = std::getenv("RT_PIPELINE");
-    return !(e && e[0] == '0');
+    if (!e || !*e) return pass_items <= kShortPassItems ? 3u : 2u;
+    const unsigned long v = std::strtoul(e, nullptr, 10);
+    return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxBufs));
 }
 
 // Segments after which waves 0-2 hand a path to the workgroup's deep wave (RT_DEEP_DEPTH;
@@ -653,14 +667,15 @@ int rt_scene_destroy(rt_scene *sc)
     (void)hipSetDevice(sc->device);
     for (auto e : sc->ev_begin) (void)hipEventDestroy(e);
     for (auto e : sc->ev_end) (void)hipEventDestroy(e);
-    for (int b = 0; b < 2; ++b) {
+    for (uint32_t b = 0; b < kMaxBufs; ++b) {
         if (sc->xs[b]) (void)hipStreamSynchronize(sc->xs[b]);
         if (sc->xs[b]) (void)hipStreamDestroy(sc->xs[b]);
         if (sc->ev_done[b]) (void)hipEventDestroy(sc->ev_done[b]);
         if (sc->ev_free[b]) (void)hipEventDestroy(sc->ev_free[b]);
     }
-    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->slots[0],
-                    (void *)sc->slots[1], (void *)sc->acc, (void *)sc->queue_ctr})
+    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr})
+        if (p) (void)hipFree(p);
+    for (float *p : sc->slots)
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
     delete sc;
@@ -734,7 +749,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     if (rc == RT_OK) {
         hipError_t e = hipMalloc((void **)&sc->queue_ctr, kCtrWords * sizeof(uint32_t));
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
-        for (int b = 0; b < 2 && rc == RT_OK; ++b) {
+        for (uint32_t b = 0; b < kMaxBufs && rc == RT_OK; ++b) {
             if (hipStreamCreateWithFlags(&sc->xs[b], hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&sc->ev_done[b], hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&sc->ev_free[b], hipEventDisableTiming) != hipSuccess)
@@ -879,12 +894,13 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
     // frames in flight: each render pass runs on internal stream xs[b] with workspace b,
     // ordered only after the caller-stream work that last read workspace b (the accumulation
-    // of the pass two before); render kernels touch no caller memory, so the caller stream sees
-    // the same results in the same order. RT_PIPELINE=0: everything on the caller stream.
-    const bool pipe = pipeline_env();
+    // of the pass `bufs` before); render kernels touch no caller memory, so the caller stream
+    // sees the same results in the same order. RT_PIPELINE=0: everything on the caller stream.
+    const uint32_t bufs = pipeline_env(n_pixels * std::min<uint64_t>(spp_pass, P.spp));
+    const bool pipe = bufs > 1;
     if (spp_pass < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
-    for (int w = 0; w < (pipe ? 2 : 1); ++w)
+    for (uint32_t w = 0; w < bufs; ++w)
         if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc)
             return rc;
     k.chunk_items = chunk_items();
@@ -896,12 +912,12 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
         // every pass takes the other workspace (and stream): pass p + 1's render overlaps pass
         // p's drain and accumulation, within a frame and across frames
-        const uint32_t wb = pipe ? sc->next_buf : 0u;
-        sc->next_buf ^= 1u;
+        const uint32_t wb = pipe ? sc->next_buf % bufs : 0u;
+        sc->next_buf = wb + 1u;
         hipStream_t xst = pipe ? sc->xs[wb] : st;
         k.slots = sc->slots[wb];
         k.queue_ctr = sc->queue_ctr + wb * 8u * rt::kQueueStride;
-        unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + 16u * rt::kQueueStride) + 4u * wb;
+        unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + kSegWords) + 4u * wb;
         k.segments = d_segments ? (pipe ? seg_b : reinterpret_cast<unsigned long long *>(d_segments)) : nullptr;
         if (pipe && sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(xst, sc->ev_free[wb], 0));
         if (pipe && d_segments) RT_HIP(hipMemsetAsync(seg_b, 0, 3 * sizeof(unsigned long long), xst));

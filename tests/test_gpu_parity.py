@@ -286,13 +286,14 @@ def test_chunking_and_passes_bit_exact(chunk, budget_samples, shade_lds, monkeyp
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("budget_samples", [0, 4])
-def test_frames_in_flight_match_serial(budget_samples, monkeypatch):
+@pytest.mark.parametrize("budget_samples,depth", [(0, "2"), (4, "2"), (0, "3"), (4, "4"), (4, "0")])
+def test_frames_in_flight_match_serial(budget_samples, depth, monkeypatch):
     """Consecutive rt_render_device calls on one scene overlap (render passes on internal
-    streams, double-buffered workspaces, alternating per pass); every frame must still equal
+    streams, RT_PIPELINE rotating workspaces, one per pass); every frame must still equal
     its serial render, with different cameras, spp and row partitions back to back and no sync
     between calls, in one pass per frame or in passes of 4 samples."""
     import torch
+    monkeypatch.setenv("RT_PIPELINE", depth)
     if budget_samples:
         monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(48 * 32 * 12 * budget_samples))
     s, m = G.scene("huge")

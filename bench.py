@@ -54,8 +54,8 @@ WORKLOAD = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--camera", default="reference", choices=["reference", "corrected"])
     ap.add_argument("--variant", default="exact", choices=["exact", "fast", "scalar"],
@@ -271,7 +271,7 @@ def main():
         }
         v = {"exact": 0, "scalar": 1, "fast": 2}[args.variant]
         cull = 0 if args.traversal == "brute" or v == 1 else int(os.environ.get("RT_CULL_STRUCTURE", "5"))
-        kname = f"render_kernel<{v}, {cull}, false>"
+        kname = f"render_kernel<{v}, {cull}, false, false>"
         pmc = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
                                             "traversal": args.traversal, "n_gpus": world})
         if pmc:

@@ -124,7 +124,7 @@ struct rt_scene {
     bool free_valid[kMaxBufs] = {};
     uint32_t next_buf = 0;  // workspace of the next render pass
     int cu_count = 0;
-    int occ[4][7][2][2];  // [variant][cull structure 0-6][deep wave][shade records in LDS] blocks per CU, -1 = unknown
+    int occ[4][8][2][2];  // [variant][cull structure 0-7][deep wave][shade records in LDS] blocks per CU, -1 = unknown
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
@@ -543,13 +543,25 @@ void fill_frame_consts(rt::KParams &k)
 // 1 = box then its spheres, cluster by cluster; 2 = every box first into per-lane masks,
 // then the wave walks the union of the masks; 3 / 4 = boxes of 2 / 4 clusters at a time
 // (loads batched), then their spheres; 5 = two levels: a box over each 4 clusters, then
-// structure 3 inside the passing ones. Default 5 (config 3: 8.4 ms; 3: 9.2-9.4; 1: 9.6-9.7).
+// structure 3 inside the passing ones (config 3 at the time: 8.4 ms; 3: 9.2-9.4; 1: 9.6-9.7);
+// 6 = structure 5's boxes into masks, then member tests compacted over the wave; 7 = structure
+// 5's walk with whole-wave control, a cluster requested by at most RT_TRANSPOSE_MAX lanes tested
+// transposed ((ray, member) pairs over the wave). Default 7 (config 3: 5.03-5.06 ms vs 5.49).
 int cull_structure()
 {
     const char *e = std::getenv("RT_CULL_STRUCTURE");
-    const int v = e ? std::atoi(e) : 5;
-    static_assert(sizeof(rt_scene::occ[0]) / sizeof(rt_scene::occ[0][0]) == 7, "occupancy cache: structures 0-6");
-    return (v >= 1 && v <= 6) ? v : 5;
+    const int v = e ? std::atoi(e) : 7;
+    static_assert(sizeof(rt_scene::occ[0]) / sizeof(rt_scene::occ[0][0]) == 8, "occupancy cache: structures 0-7");
+    return (v >= 1 && v <= 7) ? v : 7;
+}
+
+// Structure 7: a passing cluster requested by at most RT_TRANSPOSE_MAX lanes (default 16, at
+// most 16) is tested transposed, (ray, member) pairs over the whole wave; same bits either way.
+uint32_t transpose_max_env()
+{
+    const char *e = std::getenv("RT_TRANSPOSE_MAX");
+    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 16ul;
+    return static_cast<uint32_t>(std::min<unsigned long>(v, 16ul));
 }
 
 // RT_ROOT_BOX=0 disables the level-3 box gate (A/B); same bits either way.
@@ -858,6 +870,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.supers_offset = sc->supers_offset[b];
     k.use_root = root_box_env();
     k.cluster_units = sc->cluster_units;
+    k.transpose_max = transpose_max_env();
     // deep-path wave: structures 0 and 5 (RT_DEEP_DEPTH, 0 = off)
     k.deep_depth = (cull_mode == 0 || cull_mode == 5) && variant != rt::V_EXACT_SCALAR ? deep_depth_env() : 0u;
     k.shade_offset = sc->shade_offset[b];

@@ -296,10 +296,131 @@ __device__ __forceinline__ uint32_t root_gate(const KParams &p, const RayBox &rb
     return __ballot(pass) ? p.n_supers : 0u;
 }
 
+// Structure 7: the members of a passing cluster, tested transposed. A wave walks the union of
+// its lanes' passing clusters, and in structure 5 every lane then runs the cluster's 16 tests
+// while only the lanes whose segment reaches the cluster keep the results (20% of the lanes on
+// config 3). Here, when at most kTransposeMax lanes request a cluster, all 64 lanes of the wave
+// test (requesting ray, member) pairs instead — 4 rays x 16 members per round — and each
+// ray's minimum over its 16 lanes comes back to its lane. Every pair yields the reference's
+// per-sphere candidate (near root if in range, else far root, raytracer.hxx:62-90), and the
+// candidates are combined by the (t, original index) minimum as key = bits(t) << 32 | index
+// (t > 0, so the u64 order is that order): the same hit, in any order. Whole-wave code.
+constexpr uint32_t kTransposeMax = 16;  // rays per transposed cluster (KParams::transpose_max <= this)
+__device__ __forceinline__ uint64_t min16_u64(uint64_t k)  // minimum over each row of 16 lanes
+{
+    uint32_t lo = (uint32_t)k, hi = (uint32_t)(k >> 32);
+    // xor 1, xor 2 (quad permutes), then half-row mirror and row mirror: every lane of a row
+    // ends with the row's minimum
+#define RT_MIN16_STEP(ctrl)                                                                     \
+    {                                                                                           \
+        const uint32_t l2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, ctrl, 0xf, 0xf, false); \
+        const uint32_t h2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, ctrl, 0xf, 0xf, false); \
+        const bool lt = h2 < hi || (h2 == hi && l2 < lo);                                       \
+        lo = lt ? l2 : lo;                                                                      \
+        hi = lt ? h2 : hi;                                                                      \
+    }
+    RT_MIN16_STEP(0xB1)
+    RT_MIN16_STEP(0x4E)
+    RT_MIN16_STEP(0x141)
+    RT_MIN16_STEP(0x140)
+#undef RT_MIN16_STEP
+    return ((uint64_t)hi << 32) | lo;
+}
+// per-wave LDS of the transposed tests: the requesting rays by rank, and each ray's minimum
+struct TransposeLds {
+    float4 ray[kTransposeMax][2];   // {o.x, o.y, o.z, a}, {d.x, d.y, d.z, -}
+    uint64_t key[kTransposeMax];
+};
+template <bool FAST>
+__device__ __forceinline__ void members_transposed(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
+                                                   uint32_t start, uint32_t cnt, uint64_t M, bool req,
+                                                   TransposeLds *tw, f3 o, f3 d, float a, Hit &h)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t m = (uint32_t)__popcll(M);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+    if (req) {
+        tw->ray[rank][0] = make_float4(o.x, o.y, o.z, a);
+        tw->ray[rank][1] = make_float4(d.x, d.y, d.z, 0.f);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t k = lane & 15u;          // member slot (slots >= cnt read beyond: masked)
+    const bool kval = k < cnt;
+    const float4 s = geo[start + k];
+    const uint32_t sid = sidx[start + k];
+    for (uint32_t r0 = 0; r0 < m; r0 += 4u) {
+        const uint32_t r = r0 + (lane >> 4);
+        const bool valid = kval && r < m;
+        const uint32_t rr = min(r, m - 1u);
+        const float4 q0 = tw->ray[rr][0], q1 = tw->ray[rr][1];
+        const float ra = q0.w;                                              // |d|^2, as closest_hit
+        const float ocx = q0.x - s.x, ocy = q0.y - s.y, ocz = q0.z - s.z;  // raytracer.hxx:55
+        float b, disc;
+        if (FAST) {
+            b = fmaf(ocx, q1.x, fmaf(ocy, q1.y, ocz * q1.z));
+            const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -s.w)));
+            disc = fmaf(b, b, -(ra * c));
+        } else {
+            b = ocx * q1.x + ocy * q1.y + ocz * q1.z;                     // :57
+            const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;     // :58
+            disc = b * b - ra * c;                                         // :60
+        }
+        const bool pos = valid && disc > 0.f;                              // :62
+        uint64_t key = ~0ull;
+        if (__ballot(pos)) {
+            const float q = sqrtf(disc);
+            float t = (-b - q) / ra;                                       // :63
+            const bool ok = t < RT_TMAX && t > RT_TMIN;
+            if (__ballot(pos && !ok)) {
+                const float t2 = (-b + q) / ra;                            // :76
+                t = ok ? t : (t2 < RT_TMAX && t2 > RT_TMIN ? t2 : __builtin_nanf(""));
+            } else {
+                t = ok ? t : __builtin_nanf("");
+            }
+            if (pos && t == t) key = ((uint64_t)__float_as_uint(t) << 32) | sid;
+        }
+        key = min16_u64(key);
+        if (k == 0u && r < m) tw->key[r] = key;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (req) {
+        const uint64_t kk = tw->key[rank];
+        if (kk < (((uint64_t)__float_as_uint(h.t) << 32) | h.id)) {
+            h.t = __uint_as_float((uint32_t)(kk >> 32));
+            h.id = (uint32_t)kk;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <bool FAST, bool STATS>
+__device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, const float4 *__restrict__ geo,
+                                                 const uint32_t *__restrict__ sidx, TransposeLds *tw, uint32_t tmax,
+                                                 f3 o, f3 d, float a, Hit &h, Dbg &dbg, uint32_t &tests)
+{
+    const uint64_t M = __ballot(req);
+    if (!M) return;
+    const uint32_t scu = __builtin_amdgcn_readfirstlane(scu_lane);
+    const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
+    if (req) tests += cnt << 16;
+    if ((uint32_t)__popcll(M) <= tmax && cnt <= 16u) {
+        members_transposed<FAST>(geo, sidx, start, cnt, M, req, tw, o, d, a, h);
+    } else if (req) {
+        if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
+        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
+    }
+}
+
 template <bool FAST, int CULL, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
-                                           f3 d, Dbg &dbg, uint32_t &tests, uint64_t (&cmask)[2])
+                                           f3 d, Dbg &dbg, uint32_t &tests, uint64_t (&cmask)[2], bool active = true,
+                                           TransposeLds *tw = nullptr)
 {
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
     Hit h{RT_TMAX, 0xffffffffu};
@@ -323,6 +444,36 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float px = pad * aix, py = pad * aiy, pz = pad * aiz;
         const float tb_hi = h.t * 1.002f;
         const float t_lo = 0.5f * RT_TMIN;
+        if (CULL == 7) {
+            // structure 5's walk with whole-wave control (lanes predicated by `active`), so
+            // that every lane can take part in a cluster's transposed member tests
+            const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
+            const float4 *sup = clus + (p.supers_offset - p.clus_offset);
+            uint32_t n_supers = p.n_supers;
+            if (p.use_root) {
+                tests += active ? 1u : 0u;
+                if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, tb_hi)))
+                    n_supers = 0;
+            }
+            for (uint32_t g = 0; g < n_supers; ++g) {
+                const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
+                tests += active ? 1u : 0u;
+                const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t * 1.002f);
+                if (!__ballot(sp)) continue;
+                const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
+                tests += sp ? 4u : 0u;
+                for (uint32_t c = c0i; c < c0i + 4; c += 2) {
+                    const float tb_now = h.t * 1.002f;
+                    const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
+                    const bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
+                    cluster_members7<FAST, STATS>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
+                                                  dbg, tests);
+                    cluster_members7<FAST, STATS>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
+                                                  dbg, tests);
+                }
+            }
+            return h;
+        }
         if (CULL == 6) {
             // boxes only: the two-level box walk of structure 5 against the always-list t_best,
             // into a per-lane mask of passing clusters; the members are tested afterwards by
@@ -576,8 +727,13 @@ struct DeepQueue {
     uint32_t meta[kDeepQ];                // depth | pend << 8 | pend_metal << 9
 };
 
+// Structure 7 (the default) is held to 6 waves per SIMD: unhinted it takes 83 VGPRs (5 waves);
+// hinted, the allocator keeps 79 and parks one 12-byte constant that only the metal-absorption
+// path reloads (measured: 5.03-5.06 ms vs 5.19-5.24 per config-3 launch).
 template <int V, int CULL, bool STATS, bool DEEP>
-__global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(const KParams p)
+constexpr int kMinWaves = (CULL == 7 && !STATS && !DEEP) ? 6 : RT_MIN_WAVES_PER_SIMD;
+template <int V, int CULL, bool STATS, bool DEEP>
+__global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render_kernel(const KParams p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
     // Scene blob -> LDS (or read in place from global for the scalar-cache A/B variant):
@@ -617,6 +773,11 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
     // structure 6: per-wave LDS scratch of the compacted member tests (owner keys, unit list)
     uint64_t *wkey = nullptr;
     uint32_t *wlist = nullptr;
+    TransposeLds *tw = nullptr;
+    if constexpr (CULL == 7) {
+        __shared__ TransposeLds s_tw[4];
+        tw = &s_tw[threadIdx.x >> 6];
+    }
     if constexpr (CULL == 6) {
         __shared__ uint64_t s_wkey[4][64];
         __shared__ uint32_t s_wlist[4][64];
@@ -824,7 +985,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void render_kernel(cons
         Hit h{RT_TMAX, 0xffffffffu};
         uint64_t cmask[2] = {0, 0};
         uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
-        if (seg) h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, cmask);
+        if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
+            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, cmask, seg, tw);
+            if (!seg) {
+                h = Hit{RT_TMAX, 0xffffffffu};
+                tally = 0;
+            }
+        } else if (seg) {
+            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, cmask);
+        }
 #ifdef RT_DUP_HIT  // timing-only build: the closest-hit search twice on an opaque copy of the ray
         if (seg) {
             f3 o2 = o;
@@ -1259,6 +1428,7 @@ template <int V, bool STATS> static const void *ptr3(int cull, bool deep)
     if (cull == 4) return reinterpret_cast<const void *>(&render_kernel<V, 4, STATS, false>);
     if (cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS, false>);
     if (cull == 6) return reinterpret_cast<const void *>(&render_kernel<V, 6, STATS, false>);
+    if (cull == 7) return reinterpret_cast<const void *>(&render_kernel<V, 7, STATS, false>);
     return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, false>);
 }
 

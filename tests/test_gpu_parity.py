@@ -17,7 +17,7 @@ from raytracinginoneweekend_amd import _abi as abi
 pytestmark = pytest.mark.gpu
 
 RENDERS = sorted(n for n, m in G.manifest()["renders"].items() if m["rng"] == "pcg")
-VARIANTS = {"clustered": {}, "clustered2": {"_structure": "2"}, "brute": {"brute_force": True},
+VARIANTS = {"clustered": {}, "clustered2": {"_structure": "2"}, "clustered5": {"_structure": "5"}, "brute": {"brute_force": True},
             "scalar": {"scalar_scene": True}}
 
 
@@ -189,7 +189,7 @@ def _random_scene(rng, n, spread, center=(0.0, 0.0, 0.0)):
     (3, 400, 3.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
     (4, 800, 5.0, (200.0, 0.0, -150.0), abi.RT_CAMERA_CORRECTED),
 ])
-@pytest.mark.parametrize("structure", ["1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("structure", ["1", "2", "3", "4", "5", "6", "7"])
 def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, structure, monkeypatch):
     monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
     rng = np.random.default_rng(seed)
@@ -355,7 +355,7 @@ def test_cuda_impl_replacement_u8():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cluster_size", ["4", "8", "12", "24", "32", "64"])
-@pytest.mark.parametrize("structure", ["5", "6"])
+@pytest.mark.parametrize("structure", ["5", "6", "7"])
 def test_cluster_size_bit_exact(cluster_size, structure, monkeypatch):
     """Any cluster size (RT_CLUSTER_SIZE, read when the scene is created) and loop structure
     gives the oracle's bits: structure 6 deals ceil(size / 8) units of 8 members per
@@ -374,7 +374,7 @@ def test_cluster_size_bit_exact(cluster_size, structure, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("structure", ["2", "5", "6"])
+@pytest.mark.parametrize("structure", ["2", "5", "6", "7"])
 def test_many_clusters_bit_exact(structure, monkeypatch):
     """A scene with more than 128 clusters (5000 spheres): structures 2 and 6, whose per-lane
     masks hold 128 clusters, fall back to structure 5; every structure gives the oracle's bits."""

@@ -485,14 +485,29 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
             for (uint32_t g = 0; g < n_supers; ++g) {
                 const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
                 tests += active ? 1u : 0u;
-                const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t * 1.002f);
+                bool sp = active && box_pass(rb, s0, s1, t_lo, h.t * 1.002f);
+#ifdef RT_DUP_BOXES  // timing-only build: every box test twice (an opaque copy of the ray's constants)
+                {
+                    RayBox r2 = rb;
+                    asm volatile("" : "+v"(r2.ix), "+v"(r2.iy), "+v"(r2.iz), "+v"(r2.px));
+                    sp = sp && box_pass(r2, s0, s1, t_lo, h.t * 1.002f);
+                }
+#endif
                 if (!__ballot(sp)) continue;
                 const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
                 tests += sp ? 4u : 0u;
                 for (uint32_t c = c0i; c < c0i + 4; c += 2) {
                     const float tb_now = h.t * 1.002f;
                     const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
-                    const bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
+                    bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
+#ifdef RT_DUP_BOXES
+                    {
+                        RayBox r2 = rb;
+                        asm volatile("" : "+v"(r2.ix), "+v"(r2.iy), "+v"(r2.iz), "+v"(r2.px));
+                        pa = pa && box_pass(r2, a0, a1, t_lo, tb_now);
+                        pb = pb && box_pass(r2, b0, b1, t_lo, tb_now);
+                    }
+#endif
                     cluster_members7<FAST, STATS>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
                                                   dbg, tests);
                     cluster_members7<FAST, STATS>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,

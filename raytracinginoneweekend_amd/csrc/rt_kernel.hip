@@ -1122,34 +1122,36 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
                     const f3 hn = (hp - ctr) / sf.w;            // raytracer.hxx:71
                     att = att * mk(md.x, md.y, md.z);           // main.cxx:65 (unused if absorbed)
                     // raytracer.hxx:120-199
+                    o = hp;
                     if (kind == 0u) {                           // lambert, :132-141
-                        o = hp;
                         d = hp + hn;                            // + rius next iteration, then - p
                         pend = true;
                         pend_metal = false;
-                    } else if (kind == 1u) {                    // metal, :143-156
+                    } else {
+                        // metal and dielectric lanes share one unit direction and one reflection
+                        // (one code path for the wave instead of two)
                         const f3 ud = normalize(d);
-                        o = hp;
-                        d = reflect(ud, hn);                    // + rius * roughness next iteration
-                        pn = make_float4(hn.x, hn.y, hn.z, md.w);
-                        pend = true;
-                        pend_metal = true;
-                    } else {                                    // dielectric, :158-194
-                        const f3 ud = normalize(d);
-                        f3 outward = mk(-hn.x, -hn.y, -hn.z);
-                        float ri = md.w;
-                        float cosv = dot(ud, hn);
-                        if (cosv <= 0.f) {
-                            outward = outward * -1.f;
-                            ri = 1.f / ri;
-                            cosv *= -1.f;
+                        const f3 rf = reflect(ud, hn);
+                        if (kind == 1u) {                       // metal, :143-156
+                            d = rf;                             // + rius * roughness next iteration
+                            pn = make_float4(hn.x, hn.y, hn.z, md.w);
+                            pend = true;
+                            pend_metal = true;
+                        } else {                                // dielectric, :158-194
+                            f3 outward = mk(-hn.x, -hn.y, -hn.z);
+                            float ri = md.w;
+                            float cosv = dot(ud, hn);
+                            if (cosv <= 0.f) {
+                                outward = outward * -1.f;
+                                ri = 1.f / ri;
+                                cosv *= -1.f;
+                            }
+                            const f3 refr = refract(ud, outward, ri);
+                            float prob = 1.f;
+                            // length(refr) > 0 <=> norm > 0 (correctly rounded sqrt; NaN -> false)
+                            if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick(ri, cosv);
+                            d = canonical(rng, inc_data) < prob ? rf : refr;
                         }
-                        const f3 refr = refract(ud, outward, ri);
-                        float prob = 1.f;
-                        // length(refr) > 0 <=> norm > 0 (correctly rounded sqrt; NaN -> false)
-                        if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick(ri, cosv);
-                        o = hp;
-                        d = canonical(rng, inc_data) < prob ? reflect(ud, hn) : refr;
                     }
                 }
             }

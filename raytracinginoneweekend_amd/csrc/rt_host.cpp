@@ -976,7 +976,11 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         a.row_stride = k.row_stride;
         a.full_frame = k.full_frame;
         if (pipe && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
+#ifdef RT_SKIP_ACCUM  // timing-only build: no accumulation (wrong output)
+        (void)a;
+#else
         RT_HIP(rt::launch_accumulate(a, st));
+#endif
         if (pipe) {
             RT_HIP(hipEventRecord(sc->ev_free[wb], st));
             sc->free_valid[wb] = true;

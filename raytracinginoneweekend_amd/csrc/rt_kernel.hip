@@ -1138,6 +1138,22 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
                             pend = true;
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
+#ifdef RT_DUP_DIEL  // timing-only build: the dielectric shading twice on an opaque copy (result discarded)
+                            {
+                                f3 u2 = ud;
+                                asm volatile("" : "+v"(u2.x), "+v"(u2.y), "+v"(u2.z));
+                                f3 ow2 = mk(-hn.x, -hn.y, -hn.z);
+                                float ri2 = md.w, c2 = dot(u2, hn);
+                                if (c2 <= 0.f) { ow2 = ow2 * -1.f; ri2 = 1.f / ri2; c2 *= -1.f; }
+                                const f3 rr2 = refract(u2, ow2, ri2);
+                                float pr2 = 1.f;
+                                if (rr2.x * rr2.x + rr2.y * rr2.y + rr2.z * rr2.z > 0.f) pr2 = schlick(ri2, c2);
+                                uint64_t st2 = rng;
+                                asm volatile("" : "+v"(st2));
+                                const float sink = canonical(st2, inc_data) < pr2 ? rr2.x : rr2.y;
+                                asm volatile("" ::"v"(sink));
+                            }
+#endif
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w;
                             float cosv = dot(ud, hn);

@@ -52,6 +52,8 @@ struct KParams {
     uint32_t sample_begin, sample_end;      // this launch's samples
     uint32_t n_items, n_chunks, chunk_items;  // items dealt per queue grab (multiple of 64)
     uint32_t n_big_chunks;   // chunks [0, n_big_chunks) hold chunk_items items, the rest 64
+    uint32_t n_blocks;       // guided dealing: ceil(n_items / 64) blocks, 1/8 per queue
+    float guided_l2b;        // log2(beta) < 0: guided dealing (rt_kernel.hip refill); 0: fixed chunks
     // scene
     uint32_t n_spheres, n_materials;
     // scene blob, staged whole into LDS: [geo: n_geo float4 {cx, cy, cz, fl(r*r)}]

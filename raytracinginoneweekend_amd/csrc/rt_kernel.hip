@@ -908,6 +908,30 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
                 uint32_t c = 0;
                 if (lane == 0) c = atomicAdd(p.queue_ctr + q * kQueueStride, 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
+                if (p.guided_l2b < 0.f) {
+                    // guided: queue q owns blocks [qb0, qb1) of 64 items; ticket c takes blocks
+                    // [S(c), S(c+1)), S(t) = min(B, floor(B (1 - beta^t)) + 2t): chunks shrink
+                    // geometrically from ~B / (K waves per queue) to 2 blocks, so a queue is
+                    // served by few atomics and its last chunks are small. S is the same
+                    // function for every wave, so consecutive tickets tile the range; the 2t
+                    // term keeps it increasing even if exp2 or the float product is off by an
+                    // ulp (one block at most).
+                    const uint32_t qb0 = (uint32_t)(((uint64_t)p.n_blocks * q) >> 3);
+                    const uint32_t B = (uint32_t)(((uint64_t)p.n_blocks * (q + 1u)) >> 3) - qb0;
+                    auto S = [&](uint32_t t) -> uint32_t {
+                        const float x = t ? exp2f((float)t * p.guided_l2b) : 1.f;
+                        const uint64_t g = (uint64_t)floorf((float)B * (1.f - x)) + 2ull * t;
+                        return g < B ? (uint32_t)g : B;
+                    };
+                    const uint32_t s0 = S(c);
+                    if (s0 >= B) {
+                        q = (q + 1u) & 7u;
+                        if (++q_tried == 8u) exhausted = true;
+                        continue;
+                    }
+                    cnext = 64u * (qb0 + s0);
+                    cend = min(64u * (qb0 + S(c + 1u)), p.n_items);
+                } else {
                 const uint64_t chunk = (uint64_t)q + 8ull * c;
                 if (chunk >= p.n_chunks) {
                     q = (q + 1u) & 7u;
@@ -922,6 +946,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
                 } else {
                     cnext = p.n_big_chunks * p.chunk_items + ((uint32_t)chunk - p.n_big_chunks) * 64u;
                     cend = min(cnext + 64u, p.n_items);
+                }
                 }
             }
             const uint32_t avail = cend - cnext;

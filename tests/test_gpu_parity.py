@@ -267,10 +267,13 @@ def test_multi_pass_slots_bit_exact(spp, monkeypatch):
 @pytest.mark.parametrize("chunk,budget_samples,shade_lds", [(64, 0, "1"), (128, 0, "0"), (512, 0, ""), (8192, 0, "0"),
                                                            (64, 4, ""), (512, 8, "1"), (192, 12, "0")])
 def test_chunking_and_passes_bit_exact(chunk, budget_samples, shade_lds, monkeypatch):
-    """Items (one sample of one pixel) are dealt in chunks (RT_CHUNK_ITEMS), a small slot
-    budget (RT_SLOT_BUDGET_BYTES) cuts the samples into passes of a multiple of 4, and the
-    shading records may sit in LDS or global memory (RT_SHADE_LDS); none of it may change the
-    bits: the oracle's frame for spp = 23 (5 blocks of 4 + a 3-sample tail)."""
+    """Items (one sample of one pixel) are dealt in fixed chunks (RT_SCHED=fixed,
+    RT_CHUNK_ITEMS), a small slot budget (RT_SLOT_BUDGET_BYTES) cuts the samples into passes of
+    a multiple of 4, and the shading records may sit in LDS or global memory (RT_SHADE_LDS);
+    none of it may change the bits: the oracle's frame for spp = 23 (5 blocks of 4 + a 3-sample
+    tail). The default guided dealing is covered by every other test and
+    test_guided_dealing_bit_exact."""
+    monkeypatch.setenv("RT_SCHED", "fixed")
     s, m = G.scene("huge")
     W, H, spp = 40, 24, 23
     p = rt.make_params(W, H, spp, 64, 11)
@@ -410,3 +413,23 @@ def test_deep_wave_bit_exact(deep, brute, budget_samples, monkeypatch):
         want, seg = O.render_f32(s, m, cam, p)
         _bits_equal(got, want)
         assert st.segments == seg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,W,H,spp,budget_samples", [("4", 96, 40, 9, 0), ("1", 64, 33, 5, 0), ("0.25", 50, 31, 7, 0),
+                                                      ("16", 96, 40, 8, 4), ("4", 8, 8, 1, 0), ("4", 200, 100, 3, 0)])
+def test_guided_dealing_bit_exact(k, W, H, spp, budget_samples, monkeypatch):
+    """Guided dealing (the default) at several RT_GUIDED_K: each of the 8 queues owns 1/8 of the 64-item blocks and ticket t takes
+    blocks [S(t), S(t+1)), chunks shrinking geometrically to 2 blocks. Every item must be dealt
+    exactly once: the oracle's bits and segment count, in one pass or several, for tiny
+    launches (one wave) and ragged sizes."""
+    monkeypatch.setenv("RT_GUIDED_K", k)
+    if budget_samples:
+        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_samples))
+    s, m = G.scene("huge")
+    cam = O.camera_default(W, H, abi.RT_CAMERA_REFERENCE)
+    p = rt.make_params(W, H, spp, 64, 21)
+    got, st = rt.render_f32((s, m), p, cam)
+    want, seg = O.render_f32(s, m, cam, p)
+    _bits_equal(got, want)
+    assert st.segments == seg

@@ -274,7 +274,7 @@ def main():
         kname = f"render_kernel<{v}, {cull}, false, false>"
         pmc = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
                                             "traversal": args.traversal, "n_gpus": world})
-        if pmc:
+        if pmc and not rehearse:
             # HBM bytes per launch (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE) and
             # the VALU issue fraction, from the committed PMC summary of this kernel
             rec["roofline"]["traffic"] = pmc["hbm_bytes_per_launch"]

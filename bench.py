@@ -8,7 +8,7 @@ de-interleaved into the frame. Inputs (scene, camera) are resident in HBM before
 value = W*H*spp primary rays per frame * steps / max-over-ranks time (whole job).
 
 Consecutive frames are in flight together (rt_render_device runs each render kernel on an
-internal stream with a double-buffered workspace; results still land in caller-stream order),
+internal stream with its own workspace; results still land in caller-stream order),
 so ms_per_step is the steady-state frame time; frame_latency_ms is one frame alone, start to
 finish (render + accumulate + gather), timed synchronously after the timed loop.
 
@@ -88,17 +88,10 @@ def pmc_fields(path, kernel, config):
     return rec
 
 
-def pass_spp(n_pixels, spp):
-    """Samples per render pass (rt_host.cpp: a 2 GiB slot workspace, multiples of 4)."""
-    per = (1 << 31) // (n_pixels * 12)
-    return spp if per >= spp else max(4, per & ~3)
-
-
-def frames_in_flight(pass_items):
-    """Render passes in flight (RT_PIPELINE, rt_host.cpp pipeline_env: by default 3 for passes
-    of at most 32 Mi samples, else 2; at most 4)."""
+def frames_in_flight():
+    """Render passes in flight (RT_PIPELINE, rt_host.cpp pipeline_env: 3 by default, at most 4)."""
     v = os.environ.get("RT_PIPELINE", "")
-    return (3 if pass_items <= 32 << 20 else 2) if not v else max(1, min(int(v), 4))
+    return 3 if not v else max(1, min(int(v), 4))
 
 
 def cpu_baseline(cfg, camera, seed, rows, threads):
@@ -258,7 +251,7 @@ def main():
                        + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
             "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
             "frame_latency_ms": round(latency * 1e3, 3),
-            "frames_in_flight": frames_in_flight(W * rows * pass_spp(W * rows, spp)),
+            "frames_in_flight": frames_in_flight(),
             "segments_per_primary": round(segments_all / primaries, 4),
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,

@@ -64,12 +64,16 @@ hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.
 
 constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 GiB)
 // 2 x 8 queue lines, 2 x 4 u64 segment counters, then the compat kernel's pixel counter
-// workspaces for frames in flight (RT_PIPELINE = 2..kMaxBufs)
+// internal render streams for frames in flight (RT_PIPELINE = 2..kMaxBufs), and workspaces:
+// RT_WS_PER_STREAM (1..2) per stream, at most kMaxWs
 constexpr uint32_t kMaxBufs = 4;
-// counters: [kMaxBufs][8 queues x kQueueStride], then [kMaxBufs][4] u64 segment counters, then
+constexpr uint32_t kMaxWs = 2 * kMaxBufs;
+// a "short" render pass (grid_wg_per_cu): at most this many samples
+constexpr uint64_t kShortPassItems = 32ull << 20;
+// counters: [kMaxWs][8 queues x kQueueStride], then [kMaxWs][4] u64 segment counters, then
 // the compat kernel's counter
-constexpr size_t kSegWords = kMaxBufs * 8 * rt::kQueueStride;
-constexpr size_t kCompatCtr = kSegWords + kMaxBufs * 8 + 16;
+constexpr size_t kSegWords = kMaxWs * 8 * rt::kQueueStride;
+constexpr size_t kCompatCtr = kSegWords + kMaxWs * 8 + 16;
 constexpr size_t kCtrWords = kCompatCtr + rt::kQueueStride;
 
 // RT_SLOT_BUDGET_BYTES lowers the per-pass slot workspace (tests force multi-pass renders).
@@ -106,6 +110,23 @@ float guided_l2b(uint32_t total_waves)
     return static_cast<float>(std::log2(beta));
 }
 
+// Workgroups per CU of a render launch. A launch that finds no other render in flight (a
+// single frame, the first of a stream) takes the occupancy: the lowest latency. One issued
+// while earlier renders still run takes part of it, so consecutive launches run side by side
+// instead of each waiting for the previous one's workgroups to retire, and each one's drain
+// overlaps the others' bulk: (occ + 1) / 2 for passes of at most kShortPassItems samples,
+// (2 occ + 2) / 3 above. Config 3 frame stream (occupancy 6): 4 WG/CU 3.81 ms/frame, 3: 3.80-
+// 3.84 (latency 6.2 ms), 6: 3.89-3.91; 8-way row share: 3 WG/CU 0.63 ms, 2: 0.66, 4: 0.66,
+// 6: 0.68. RT_GRID_WG_PER_CU=n fixes it (A/B).
+int grid_wg_per_cu(int occ, bool in_flight, uint64_t pass_items)
+{
+    const char *e = std::getenv("RT_GRID_WG_PER_CU");
+    const long v = e && *e ? std::strtol(e, nullptr, 10) : 0;
+    if (v > 0) return std::min<int>(occ, static_cast<int>(v));
+    if (!in_flight) return occ;
+    return std::max(1, pass_items <= kShortPassItems ? (occ + 1) / 2 : (2 * occ + 2) / 3);
+}
+
 // Share of a launch's items dealt in 64-item chunks at its end (RT_TAIL_PCT for A/B, 0-100).
 uint32_t tail_pct()
 {
@@ -131,15 +152,16 @@ struct rt_scene {
     // workspaces: consecutive render passes (of one frame or of consecutive frames) rotate over
     // internal streams xs[b] and workspaces slots[b], so a pass renders while the caller stream
     // still accumulates the previous ones
-    float *slots[kMaxBufs] = {};
-    size_t slots_bytes[kMaxBufs] = {};
+    float *slots[kMaxWs] = {};
+    size_t slots_bytes[kMaxWs] = {};
     float *acc = nullptr;
     size_t acc_bytes = 0;
     uint32_t *queue_ctr = nullptr;  // kCtrWords: queue and segment counters (layout at kCtrWords)
     hipStream_t xs[kMaxBufs] = {};
-    hipEvent_t ev_done[kMaxBufs] = {}, ev_free[kMaxBufs] = {};
-    bool free_valid[kMaxBufs] = {};
+    hipEvent_t ev_done[kMaxWs] = {}, ev_free[kMaxWs] = {};
+    bool free_valid[kMaxWs] = {};
     uint32_t next_buf = 0;  // workspace of the next render pass
+    int last_ws = -1;       // workspace of the last render pass issued (its ev_done), -1 = none
     int cu_count = 0;
     int occ[4][8][2][2];  // [variant][cull structure 0-7][deep wave][shade records in LDS] blocks per CU, -1 = unknown
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
@@ -601,19 +623,32 @@ int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, flo
                   uint64_t *d_segments);
 
 // Render passes in flight: RT_PIPELINE=0 (or 1) runs the render kernels on the caller stream;
-// 2..kMaxBufs rotate that many internal streams and workspaces. Default: 3 for passes of at
-// most kShortPassItems samples, whose launch is short next to its drain (the max-depth paths
-// take the same ~64 iterations whatever the pass size; measured on an 8-way row share of
-// config 3, 14.7 M samples: 0.77 ms/frame with 3 vs 0.84 with 2), else 2 (no gain measured on
-// full frames, and each render's own duration stays close to a launch alone). 4 is not faster:
-// with the caller's stream that is more streams than the process's 4 hardware queues.
-constexpr uint64_t kShortPassItems = 32ull << 20;
+// 2..kMaxBufs rotate that many internal streams. Default 3: the max-depth paths give every
+// launch a drain of ~64 iterations whatever its size, and with 3 streams (and partial grids,
+// grid_wg_per_cu) two other renders fill the machine while one drains. Measured on config 3
+// (frame stream): 3.81-3.83 ms/frame with 3 streams vs 3.90-3.93 with 2; an 8-way row share
+// (14.7 M samples) 0.63 vs 0.68. 4 is not faster: with the caller's stream that is more
+// streams than the process's 4 hardware queues.
 uint32_t pipeline_env(uint64_t pass_items)
 {
     const char *e = std::getenv("RT_PIPELINE");
-    if (!e || !*e) return pass_items <= kShortPassItems ? 3u : 2u;
+    (void)pass_items;
+    if (!e || !*e) return 3u;
     const unsigned long v = std::strtoul(e, nullptr, 10);
     return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxBufs));
+}
+
+// Workspaces per internal stream (RT_WS_PER_STREAM, 1..2; default 2). Pass p renders on stream
+// p % streams into workspace p % (streams x this): with 2, the render that next takes a stream
+// waits only for that stream's previous render (stream order), not for the accumulation of
+// the pass that last used its workspace, which runs on the caller stream and, beside the
+// running renders, waits for free CU slots.
+uint32_t ws_per_stream_env()
+{
+    const char *e = std::getenv("RT_WS_PER_STREAM");
+    if (!e || !*e) return 2u;
+    const unsigned long v = std::strtoul(e, nullptr, 10);
+    return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxWs / kMaxBufs));
 }
 
 // Segments after which waves 0-2 hand a path to the workgroup's deep wave (RT_DEEP_DEPTH;
@@ -699,6 +734,8 @@ int rt_scene_destroy(rt_scene *sc)
     for (uint32_t b = 0; b < kMaxBufs; ++b) {
         if (sc->xs[b]) (void)hipStreamSynchronize(sc->xs[b]);
         if (sc->xs[b]) (void)hipStreamDestroy(sc->xs[b]);
+    }
+    for (uint32_t b = 0; b < kMaxWs; ++b) {
         if (sc->ev_done[b]) (void)hipEventDestroy(sc->ev_done[b]);
         if (sc->ev_free[b]) (void)hipEventDestroy(sc->ev_free[b]);
     }
@@ -778,8 +815,8 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     if (rc == RT_OK) {
         hipError_t e = hipMalloc((void **)&sc->queue_ctr, kCtrWords * sizeof(uint32_t));
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
-        for (uint32_t b = 0; b < kMaxBufs && rc == RT_OK; ++b) {
-            if (hipStreamCreateWithFlags(&sc->xs[b], hipStreamNonBlocking) != hipSuccess ||
+        for (uint32_t b = 0; b < kMaxWs && rc == RT_OK; ++b) {
+            if ((b < kMaxBufs && hipStreamCreateWithFlags(&sc->xs[b], hipStreamNonBlocking) != hipSuccess) ||
                 hipEventCreateWithFlags(&sc->ev_done[b], hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&sc->ev_free[b], hipEventDisableTiming) != hipSuccess)
                 rc = fail(RT_ERR_DEVICE, "rt_scene_create: stream/event creation failed");
@@ -922,15 +959,17 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     if (spp_pass == 0) spp_pass = 4;
     if (n_pixels * std::min<uint64_t>(spp_pass, P.spp) >= (1ull << 31) - 8192)
         return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
-    // frames in flight: each render pass runs on internal stream xs[b] with workspace b,
-    // ordered only after the caller-stream work that last read workspace b (the accumulation
-    // of the pass `bufs` before); render kernels touch no caller memory, so the caller stream
-    // sees the same results in the same order. RT_PIPELINE=0: everything on the caller stream.
+    // frames in flight: render pass p runs on internal stream xs[p % bufs] with workspace
+    // w = p % n_ws, ordered after that stream's previous render and after the caller-stream
+    // work that last read workspace w (the accumulation of pass p - n_ws); render kernels
+    // touch no caller memory, so the caller stream sees the same results in the same order.
+    // RT_PIPELINE=0: everything on the caller stream.
     const uint32_t bufs = pipeline_env(n_pixels * std::min<uint64_t>(spp_pass, P.spp));
     const bool pipe = bufs > 1;
+    const uint32_t n_ws = pipe ? bufs * ws_per_stream_env() : 1u;
     if (spp_pass < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
-    for (uint32_t w = 0; w < bufs; ++w)
+    for (uint32_t w = 0; w < n_ws; ++w)
         if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc)
             return rc;
     k.chunk_items = chunk_items();
@@ -942,9 +981,11 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
         // every pass takes the other workspace (and stream): pass p + 1's render overlaps pass
         // p's drain and accumulation, within a frame and across frames
-        const uint32_t wb = pipe ? sc->next_buf % bufs : 0u;
+        const uint32_t wb = pipe ? sc->next_buf % n_ws : 0u;
         sc->next_buf = wb + 1u;
-        hipStream_t xst = pipe ? sc->xs[wb] : st;
+        hipStream_t xst = pipe ? sc->xs[wb % bufs] : st;
+        // another render still running? (then this one takes a partial grid, grid_wg_per_cu)
+        const bool in_flight = pipe && sc->last_ws >= 0 && hipEventQuery(sc->ev_done[sc->last_ws]) == hipErrorNotReady;
         k.slots = sc->slots[wb];
         k.queue_ctr = sc->queue_ctr + wb * 8u * rt::kQueueStride;
         unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + kSegWords) + 4u * wb;
@@ -963,7 +1004,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
             k.n_chunks = k.n_big_chunks + (rest + 63u) / 64u;
         }
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(occ) * sc->cu_count, (k.n_items + 255u) / 256u)));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u);
         RT_HIP(hipMemsetAsync(k.queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), xst));
@@ -978,6 +1019,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         if (pipe) {
             RT_HIP(hipEventRecord(sc->ev_done[wb], xst));
             RT_HIP(hipStreamWaitEvent(st, sc->ev_done[wb], 0));
+            sc->last_ws = static_cast<int>(wb);
         }
         rt::KAccum a{};
         a.slots = sc->slots[wb];

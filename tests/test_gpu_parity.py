@@ -289,14 +289,19 @@ def test_chunking_and_passes_bit_exact(chunk, budget_samples, shade_lds, monkeyp
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("budget_samples,depth", [(0, "2"), (4, "2"), (0, "3"), (4, "4"), (4, "0")])
-def test_frames_in_flight_match_serial(budget_samples, depth, monkeypatch):
-    """Consecutive rt_render_device calls on one scene overlap (render passes on internal
-    streams, RT_PIPELINE rotating workspaces, one per pass); every frame must still equal
-    its serial render, with different cameras, spp and row partitions back to back and no sync
-    between calls, in one pass per frame or in passes of 4 samples."""
+@pytest.mark.parametrize("budget_samples,depth,ws,grid", [
+    (0, "2", "1", ""), (4, "2", "1", ""), (0, "3", "2", ""), (4, "3", "2", ""), (4, "4", "2", "2"),
+    (0, "3", "1", "1"), (4, "0", "2", "")])
+def test_frames_in_flight_match_serial(budget_samples, depth, ws, grid, monkeypatch):
+    """Consecutive rt_render_device calls on one scene overlap (render passes on RT_PIPELINE
+    internal streams, RT_WS_PER_STREAM workspaces per stream, partial grids while other renders
+    run); every frame must still equal its serial render, with different cameras, spp and row
+    partitions back to back and no sync between calls, in one pass per frame or in passes of 4
+    samples."""
     import torch
     monkeypatch.setenv("RT_PIPELINE", depth)
+    monkeypatch.setenv("RT_WS_PER_STREAM", ws)
+    monkeypatch.setenv("RT_GRID_WG_PER_CU", grid)
     if budget_samples:
         monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(48 * 32 * 12 * budget_samples))
     s, m = G.scene("huge")

@@ -92,8 +92,12 @@ struct KAccum {
     uint32_t first, last, spp;
     uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame;
     // frames in flight: thread 0 adds the render's internal segment counters to the caller's
-    const unsigned long long *seg_from;
+    // and zeroes them
+    unsigned long long *seg_from;
     unsigned long long *seg_to;
+    // the render's queue counters, zeroed here for the next render on this workspace
+    uint32_t *queue_reset;
+    uint32_t queue_words;
 };
 
 // RT_FLAG_CUDA_COMPAT: the semantics of the reference's CUDA variant (src/CUDA/cuda_impl.cu),

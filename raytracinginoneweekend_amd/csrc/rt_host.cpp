@@ -68,8 +68,6 @@ constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 G
 // RT_WS_PER_STREAM (1..2) per stream, at most kMaxWs
 constexpr uint32_t kMaxBufs = 4;
 constexpr uint32_t kMaxWs = 2 * kMaxBufs;
-// a "short" render pass (grid_wg_per_cu): at most this many samples
-constexpr uint64_t kShortPassItems = 32ull << 20;
 // counters: [kMaxWs][8 queues x kQueueStride], then [kMaxWs][4] u64 segment counters, then
 // the compat kernel's counter
 constexpr size_t kSegWords = kMaxWs * 8 * rt::kQueueStride;
@@ -112,19 +110,19 @@ float guided_l2b(uint32_t total_waves)
 
 // Workgroups per CU of a render launch. A launch that finds no other render in flight (a
 // single frame, the first of a stream) takes the occupancy: the lowest latency. One issued
-// while earlier renders still run takes part of it, so consecutive launches run side by side
-// instead of each waiting for the previous one's workgroups to retire, and each one's drain
-// overlaps the others' bulk: (occ + 1) / 2 for passes of at most kShortPassItems samples,
-// (2 occ + 2) / 3 above. Config 3 frame stream (occupancy 6): 4 WG/CU 3.81 ms/frame, 3: 3.80-
-// 3.84 (latency 6.2 ms), 6: 3.89-3.91; 8-way row share: 3 WG/CU 0.63 ms, 2: 0.66, 4: 0.66,
-// 6: 0.68. RT_GRID_WG_PER_CU=n fixes it (A/B).
-int grid_wg_per_cu(int occ, bool in_flight, uint64_t pass_items)
+// while earlier renders still run takes half of it, (occ + 1) / 2, so consecutive launches run
+// side by side instead of each waiting for the previous one's workgroups to retire, and each
+// one's drain overlaps the others' bulk. Measured (occupancy 6, in-flight grid 3 / 4 / 6):
+// config 3 frame stream 3.80-3.92 / 3.81-3.88 / 3.89-3.93 ms; 2-way row share 1.97-2.01 /
+// 2.03-2.05 / 2.08; 8-way row share 0.63 / 0.66 / 0.68 (2: 0.66); configs 4 and 5 equal.
+// RT_GRID_WG_PER_CU=n sets the in-flight grid (A/B).
+int grid_wg_per_cu(int occ, bool in_flight)
 {
+    if (!in_flight) return occ;
     const char *e = std::getenv("RT_GRID_WG_PER_CU");
     const long v = e && *e ? std::strtol(e, nullptr, 10) : 0;
     if (v > 0) return std::min<int>(occ, static_cast<int>(v));
-    if (!in_flight) return occ;
-    return std::max(1, pass_items <= kShortPassItems ? (occ + 1) / 2 : (2 * occ + 2) / 3);
+    return std::max(1, (occ + 1) / 2);
 }
 
 // Share of a launch's items dealt in 64-item chunks at its end (RT_TAIL_PCT for A/B, 0-100).
@@ -160,6 +158,9 @@ struct rt_scene {
     hipStream_t xs[kMaxBufs] = {};
     hipEvent_t ev_done[kMaxWs] = {}, ev_free[kMaxWs] = {};
     bool free_valid[kMaxWs] = {};
+    // queue/segment counters of workspace b not known to be zero (set while a render using
+    // them is enqueued, cleared once the accumulation that resets them is enqueued after it)
+    bool ctr_dirty[kMaxWs] = {true, true, true, true, true, true, true, true};
     uint32_t next_buf = 0;  // workspace of the next render pass
     int last_ws = -1;       // workspace of the last render pass issued (its ev_done), -1 = none
     int cu_count = 0;
@@ -629,10 +630,9 @@ int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, flo
 // (frame stream): 3.81-3.83 ms/frame with 3 streams vs 3.90-3.93 with 2; an 8-way row share
 // (14.7 M samples) 0.63 vs 0.68. 4 is not faster: with the caller's stream that is more
 // streams than the process's 4 hardware queues.
-uint32_t pipeline_env(uint64_t pass_items)
+uint32_t pipeline_env()
 {
     const char *e = std::getenv("RT_PIPELINE");
-    (void)pass_items;
     if (!e || !*e) return 3u;
     const unsigned long v = std::strtoul(e, nullptr, 10);
     return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxBufs));
@@ -964,7 +964,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     // work that last read workspace w (the accumulation of pass p - n_ws); render kernels
     // touch no caller memory, so the caller stream sees the same results in the same order.
     // RT_PIPELINE=0: everything on the caller stream.
-    const uint32_t bufs = pipeline_env(n_pixels * std::min<uint64_t>(spp_pass, P.spp));
+    const uint32_t bufs = pipeline_env();
     const bool pipe = bufs > 1;
     const uint32_t n_ws = pipe ? bufs * ws_per_stream_env() : 1u;
     if (spp_pass < P.spp)
@@ -979,7 +979,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     for (uint32_t s0 = 0; s0 < P.spp; s0 += static_cast<uint32_t>(spp_pass)) {
         const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
-        // every pass takes the other workspace (and stream): pass p + 1's render overlaps pass
+        // every pass takes the next workspace and stream: pass p + 1's render overlaps pass
         // p's drain and accumulation, within a frame and across frames
         const uint32_t wb = pipe ? sc->next_buf % n_ws : 0u;
         sc->next_buf = wb + 1u;
@@ -991,7 +991,11 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + kSegWords) + 4u * wb;
         k.segments = d_segments ? (pipe ? seg_b : reinterpret_cast<unsigned long long *>(d_segments)) : nullptr;
         if (pipe && sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(xst, sc->ev_free[wb], 0));
-        if (pipe && d_segments) RT_HIP(hipMemsetAsync(seg_b, 0, 3 * sizeof(unsigned long long), xst));
+        if (sc->ctr_dirty[wb]) {
+            RT_HIP(hipMemsetAsync(k.queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), xst));
+            RT_HIP(hipMemsetAsync(seg_b, 0, 3 * sizeof(unsigned long long), xst));
+        }
+        sc->ctr_dirty[wb] = true;
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], xst));
         k.sample_begin = s0;
         k.sample_end = s1;
@@ -1004,10 +1008,9 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
             k.n_chunks = k.n_big_chunks + (rest + 63u) / 64u;
         }
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u);
-        RT_HIP(hipMemsetAsync(k.queue_ctr, 0, 8 * rt::kQueueStride * sizeof(uint32_t), xst));
         if (verbose())
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) %s%u\n",
                          variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1,
@@ -1039,10 +1042,13 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         a.row_stride = k.row_stride;
         a.full_frame = k.full_frame;
         if (pipe && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
+        a.queue_reset = k.queue_ctr;
+        a.queue_words = 8 * rt::kQueueStride;
 #ifdef RT_SKIP_ACCUM  // timing-only build: no accumulation (wrong output)
         (void)a;
 #else
         RT_HIP(rt::launch_accumulate(a, st));
+        sc->ctr_dirty[wb] = false;
 #endif
         if (pipe) {
             RT_HIP(hipEventRecord(sc->ev_free[wb], st));

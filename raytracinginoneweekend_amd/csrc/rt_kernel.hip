@@ -1472,7 +1472,14 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0 && k.seg_to)
-        for (int c = 0; c < 3; ++c) k.seg_to[c] += k.seg_from[c];
+        for (int c = 0; c < 3; ++c) {
+            k.seg_to[c] += k.seg_from[c];
+            k.seg_from[c] = 0ull;
+        }
+    // the render that used this workspace has finished: reset its queue counters (no memset
+    // kernel in front of the next render)
+    if (k.queue_reset)
+        for (uint32_t w = i; w < k.queue_words; w += gridDim.x * blockDim.x) k.queue_reset[w] = 0u;
     if (i >= k.n_pixels) return;
     f3 acc;
     if (k.first) acc = mk(0.f, 0.f, 0.f);

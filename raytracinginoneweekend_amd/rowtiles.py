@@ -30,16 +30,19 @@ class FrameGather:
     def __init__(self, tile, world, rank, group=None):
         self.world, self.rank, self.group = world, rank, group
         self.rows, self.width = tile.shape[0], tile.shape[1]
-        self.parts = [torch.empty_like(tile) for _ in range(world)] if rank == 0 and world > 1 else None
+        # rank 0 gathers the tiles into one (world, rows, W, 3) buffer (each part a contiguous
+        # slice of it), then de-interleaves it into the frame with ONE strided copy
+        self.gathered = torch.empty((world, self.rows, self.width, 3), dtype=tile.dtype, device=tile.device) \
+            if rank == 0 and world > 1 else None
+        self.parts = list(self.gathered.unbind(0)) if self.gathered is not None else None
         self.frame = torch.empty((self.rows * world, self.width, 3), dtype=tile.dtype, device=tile.device) \
-            if rank == 0 else None
+            if rank == 0 and world > 1 else None
 
     def __call__(self, tile):
-        if self.world == 1:
-            self.frame.copy_(tile)
-            return self.frame
+        if self.world == 1:  # the one tile is the frame
+            return tile
         dist.gather(tile, gather_list=self.parts, dst=0, group=self.group)
         if self.rank == 0:
             # frame row y = i*world + r  <-  tile r row i
-            self.frame.view(self.rows, self.world, self.width, 3).copy_(torch.stack(self.parts, dim=1))
+            self.frame.view(self.rows, self.world, self.width, 3).copy_(self.gathered.transpose(0, 1))
         return self.frame

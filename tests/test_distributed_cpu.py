@@ -39,7 +39,7 @@ def _worker(rank, world, port, W, H, spp, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_row_tiles_gather_bitwise(tmp_path, world):
     W, H, spp = 48, 24, 2
     out = str(tmp_path / "frame.npy")

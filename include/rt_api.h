@@ -182,11 +182,11 @@ int rt_scene_destroy(rt_scene *scene);
 /* Enqueue one render for `stream` (a hipStream_t, or NULL for the null stream).
  * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64[3]
  * that accumulates {segments, sphere tests, cluster box tests} (zero it first). No
- * host sync. The render kernels rotate over 2 internal streams of the scene, each with its
- * own workspace (3 for passes of at most 32 Mi samples), so consecutive frames overlap; they
- * read only the scene and the by-value arguments, and the writes to d_rgb / d_segments are
- * enqueued on `stream`, so results appear in stream order (RT_PIPELINE=n in the environment
- * sets the depth, 2..4; 0: all on `stream`).                                                 */
+ * host sync. The render kernels rotate over 3 internal streams of the scene and 6 slot
+ * workspaces, so consecutive frames overlap; they read only the scene and the by-value
+ * arguments, and the writes to d_rgb / d_segments are enqueued on `stream`, so results appear
+ * in stream order (RT_PIPELINE=n in the environment sets the streams, 2..4; 0: all on
+ * `stream`).                                                                                 */
 int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
                      float *d_rgb, void *stream, uint64_t *d_segments);
 /* Durations (ms, HIP events on the render kernels' stream) of the render kernel launches of the

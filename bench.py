@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--rehearse-world", type=int, default=0,
                     help="diagnostic, 1 GPU: render only rank 0's rows of an N-way split (no gather) to "
                          "estimate one rank's frame time at N GPUs; not a bench line")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = leave the environment): "
+                         "the library runs one render stream fewer than this, 2..4 (rt_host.cpp pipeline_env)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_render_c3.json"),
                     help="PMC summary of this kernel (scripts/pmc_round.sh) for roofline.traffic / VALU busy")
     return ap.parse_args()
@@ -89,9 +92,12 @@ def pmc_fields(path, kernel, config):
 
 
 def frames_in_flight():
-    """Render passes in flight (RT_PIPELINE, rt_host.cpp pipeline_env: 3 by default, at most 4)."""
+    """Render streams (RT_PIPELINE, rt_host.cpp pipeline_env: by default GPU_MAX_HW_QUEUES - 1,
+    within 2..4)."""
     v = os.environ.get("RT_PIPELINE", "")
-    return 3 if not v else max(1, min(int(v), 4))
+    if v:
+        return max(1, min(int(v), 4))
+    return max(2, min(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) - 1, 4))
 
 
 def cpu_baseline(cfg, camera, seed, rows, threads):
@@ -139,6 +145,8 @@ def cpu_baseline(cfg, camera, seed, rows, threads):
 
 def main():
     args = parse()
+    if args.hw_queues > 0:  # before anything starts HIP
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import torch.distributed as dist
 
@@ -252,7 +260,8 @@ def main():
                        "width": W, "height": H, "spp": spp, "max_depth": depth, "camera": args.camera,
                        "kernel": "compat_kernel (cuda_impl.cu semantics, bit-exact vs its restatement)" if compat else
                        ("fast (FMA, stated tolerance)" if args.variant == "fast" else f"{args.variant} (bit-exact)")
-                       + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather"},
+                       + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather",
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
             "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
             "frame_latency_ms": round(latency * 1e3, 3),
             "frames_in_flight": frames_in_flight(),

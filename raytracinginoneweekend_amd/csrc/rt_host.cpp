@@ -112,17 +112,20 @@ float guided_l2b(uint32_t total_waves)
 // single frame, the first of a stream) takes the occupancy: the lowest latency. One issued
 // while earlier renders still run takes half of it, (occ + 1) / 2, so consecutive launches run
 // side by side instead of each waiting for the previous one's workgroups to retire, and each
-// one's drain overlaps the others' bulk. Measured (occupancy 6, in-flight grid 3 / 4 / 6):
+// one's drain overlaps the others' bulk; with n render streams, ceil(occ / (n - 1)) (3 streams:
+// half; 4 streams: a third). Measured with 3 streams (occupancy 6, in-flight grid 3 / 4 / 6):
 // config 3 frame stream 3.80-3.92 / 3.81-3.88 / 3.89-3.93 ms; 2-way row share 1.97-2.01 /
 // 2.03-2.05 / 2.08; 8-way row share 0.63 / 0.66 / 0.68 (2: 0.66); configs 4 and 5 equal.
-// RT_GRID_WG_PER_CU=n sets the in-flight grid (A/B).
-int grid_wg_per_cu(int occ, bool in_flight)
+// With 4 streams (GPU_MAX_HW_QUEUES=8): grid 2: config 3 3.83-3.84 ms, 8-way 0.61; grid 3:
+// 3.84-3.86, 0.65. RT_GRID_WG_PER_CU=n sets the in-flight grid (A/B).
+int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams)
 {
     if (!in_flight) return occ;
     const char *e = std::getenv("RT_GRID_WG_PER_CU");
     const long v = e && *e ? std::strtol(e, nullptr, 10) : 0;
     if (v > 0) return std::min<int>(occ, static_cast<int>(v));
-    return std::max(1, (occ + 1) / 2);
+    const int others = std::max(1, static_cast<int>(streams) - 1);
+    return std::max(1, (occ + others - 1) / others);
 }
 
 // Share of a launch's items dealt in 64-item chunks at its end (RT_TAIL_PCT for A/B, 0-100).
@@ -624,16 +627,21 @@ int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, flo
                   uint64_t *d_segments);
 
 // Render passes in flight: RT_PIPELINE=0 (or 1) runs the render kernels on the caller stream;
-// 2..kMaxBufs rotate that many internal streams. Default 3: the max-depth paths give every
-// launch a drain of ~64 iterations whatever its size, and with 3 streams (and partial grids,
-// grid_wg_per_cu) two other renders fill the machine while one drains. Measured on config 3
-// (frame stream): 3.81-3.83 ms/frame with 3 streams vs 3.90-3.93 with 2; an 8-way row share
-// (14.7 M samples) 0.63 vs 0.68. 4 is not faster: with the caller's stream that is more
-// streams than the process's 4 hardware queues.
+// 2..kMaxBufs rotate that many internal streams. Default: one stream fewer than the process's
+// hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4; the caller's stream takes one), 2..4.
+// The max-depth paths give every launch a drain of ~64 iterations whatever its size; with 3
+// streams (and partial grids, grid_wg_per_cu) two other renders fill the machine while one
+// drains. Measured on config 3 (frame stream): 3.81-3.87 ms/frame with 3 streams vs 3.90-3.93
+// with 2; an 8-way row share (14.7 M samples) 0.63-0.64 vs 0.68; 4 streams on 8 hardware
+// queues: 3.83-3.84 and 0.61. More streams than hardware queues share queues and serialise.
 uint32_t pipeline_env()
 {
     const char *e = std::getenv("RT_PIPELINE");
-    if (!e || !*e) return 3u;
+    if (!e || !*e) {
+        const char *q = std::getenv("GPU_MAX_HW_QUEUES");
+        const unsigned long hw = q && *q ? std::strtoul(q, nullptr, 10) : 4ul;
+        return static_cast<uint32_t>(std::clamp<unsigned long>(hw > 1 ? hw - 1 : 1, 2, kMaxBufs));
+    }
     const unsigned long v = std::strtoul(e, nullptr, 10);
     return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxBufs));
 }
@@ -1008,7 +1016,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
             k.n_chunks = k.n_big_chunks + (rest + 63u) / 64u;
         }
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight)) * sc->cu_count, (k.n_items + 255u) / 256u)));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u);
         if (verbose())

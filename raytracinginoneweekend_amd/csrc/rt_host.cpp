@@ -112,19 +112,24 @@ float guided_l2b(uint32_t total_waves)
 // single frame, the first of a stream) takes the occupancy: the lowest latency. One issued
 // while earlier renders still run takes half of it, (occ + 1) / 2, so consecutive launches run
 // side by side instead of each waiting for the previous one's workgroups to retire, and each
-// one's drain overlaps the others' bulk; with n render streams, ceil(occ / (n - 1)) (3 streams:
-// half; 4 streams: a third). Measured with 3 streams (occupancy 6, in-flight grid 3 / 4 / 6):
+// one's drain overlaps the others' bulk: half the occupancy, and for passes of at most
+// kShortPassItems samples with n render streams ceil(occ / (n - 1)) (4 streams: a third).
+// Measured with 3 streams (occupancy 6, in-flight grid 3 / 4 / 6):
 // config 3 frame stream 3.80-3.92 / 3.81-3.88 / 3.89-3.93 ms; 2-way row share 1.97-2.01 /
 // 2.03-2.05 / 2.08; 8-way row share 0.63 / 0.66 / 0.68 (2: 0.66); configs 4 and 5 equal.
-// With 4 streams (GPU_MAX_HW_QUEUES=8): grid 2: config 3 3.83-3.84 ms, 8-way 0.61; grid 3:
-// 3.84-3.86, 0.65. RT_GRID_WG_PER_CU=n sets the in-flight grid (A/B).
-int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams)
+// With 4 streams (GPU_MAX_HW_QUEUES=8): grid 2: config 3 3.83-3.84 ms, 8-way 0.60-0.61; grid
+// 3: 3.84-3.86, 0.65 — but config 3 with the corrected camera (7 segments per primary, 29 ms
+// frames) 32.0-34.3 ms at grid 2 vs 29.8 at grid 3 (28.8 with 2 streams and full grids), so
+// the third applies to short passes only. RT_GRID_WG_PER_CU=n sets the in-flight grid (A/B).
+constexpr uint64_t kShortPassItems = 32ull << 20;
+int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams, uint64_t pass_items)
 {
     if (!in_flight) return occ;
     const char *e = std::getenv("RT_GRID_WG_PER_CU");
     const long v = e && *e ? std::strtol(e, nullptr, 10) : 0;
     if (v > 0) return std::min<int>(occ, static_cast<int>(v));
-    const int others = std::max(1, static_cast<int>(streams) - 1);
+    const int others = pass_items <= kShortPassItems ? std::max(1, static_cast<int>(streams) - 1)
+                                                     : std::min(2, std::max(1, static_cast<int>(streams) - 1));
     return std::max(1, (occ + others - 1) / others);
 }
 
@@ -1016,7 +1021,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
             k.n_chunks = k.n_big_chunks + (rest + 63u) / 64u;
         }
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs)) * sc->cu_count, (k.n_items + 255u) / 256u)));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u);
         if (verbose())

@@ -8,7 +8,8 @@ namespace rt {
 
 // Work decomposition:
 //   pixel enumeration i in [0, n_pixels): the rows of this render (y = row_offset + rr*row_stride),
-//     in 8x8 tiles while both W and the row count allow, row-major for the remainder;
+//     in 64-pixel tiles (2^tile_lw x 64/2^tile_lw) while W and the row count allow, row-major
+//     for the remainder;
 //   a work item is one sample of one pixel: a lane traces it and stores its colour to the
 //     sample's slot [s - sample_begin][i]. The reference averages samples with libstdc++'s
 //     blocked reduce (<numeric>:443-460), ((c0+c1)+(c2+c3)) per block of 4, blocks in order,
@@ -34,6 +35,7 @@ struct FrameConsts {
     uint32_t inc_data_lo, inc_data_hi, inc_cam_lo, inc_cam_hi;
     uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, sample_begin;
     UDiv div_W, div_tiles_x, div_n_pixels;
+    uint32_t tile_lw;  // log2 of the tile width (3..6): tiles of 2^lw x 64/2^lw pixels
 };
 
 struct KParams {
@@ -48,7 +50,8 @@ struct KParams {
     uint32_t full_frame;
     uint64_t inc_data, inc_cam;  // PCG increments: ((2*seed) << 1) | 1 and ((2*seed+1) << 1) | 1
     // decomposition
-    uint32_t n_pixels, tiles_x, tiled_rows;  // tiled_rows: rows covered by 8x8 tiles (0 = untiled)
+    uint32_t n_pixels, tiles_x, tiled_rows;  // tiled_rows: rows covered by 64-pixel tiles (0 = untiled)
+    uint32_t tile_lw;                       // log2 of the tile width (3: 8x8, 4: 16x4, 5: 32x2, 6: 64x1)
     uint32_t sample_begin, sample_end;      // this launch's samples
     uint32_t n_items, n_chunks, chunk_items;  // items dealt per queue grab (multiple of 64)
     uint32_t n_big_chunks;   // chunks [0, n_big_chunks) hold chunk_items items, the rest 64
@@ -90,7 +93,7 @@ struct KAccum {
     uint32_t n_pixels, n_samples;
     uint32_t n_blocks;       // full blocks of 4 among this pass's samples (the rest is the tail)
     uint32_t first, last, spp;
-    uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame;
+    uint32_t W, tiles_x, tiled_rows, row_offset, row_stride, full_frame, tile_lw;
     // frames in flight: thread 0 adds the render's internal segment counters to the caller's
     // and zeroes them
     unsigned long long *seg_from;

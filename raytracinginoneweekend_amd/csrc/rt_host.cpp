@@ -108,6 +108,20 @@ float guided_l2b(uint32_t total_waves)
     return static_cast<float>(std::log2(beta));
 }
 
+// log2 of the tile width (RT_TILE_LW=3..6 for A/B; default 3 = 8x8 tiles). Tiles whose image
+// footprint stays near square for strided rows (16x4 at stride 2-4, 32x2 at 5-8) were not
+// faster: row shares of config 3 at N = 8: 8x8 0.61-0.62 ms, 32x2 0.62, 64x1 0.66; N = 4:
+// 8x8 1.08-1.10, 16x4 1.10, 32x2 1.14; N = 2: 8x8 1.99, 16x4 2.02-2.05.
+uint32_t tile_lw_for(uint32_t width, uint32_t stride)
+{
+    (void)stride;
+    const char *e = std::getenv("RT_TILE_LW");
+    uint32_t lw = 3u;
+    if (e && *e) lw = static_cast<uint32_t>(std::clamp<long>(std::strtol(e, nullptr, 10), 3, 6));
+    while (lw > 3 && width % (1u << lw)) --lw;  // the tile width must divide the row
+    return lw;
+}
+
 // Workgroups per CU of a render launch. A launch that finds no other render in flight (a
 // single frame, the first of a stream) takes the occupancy: the lowest latency. One issued
 // while earlier renders still run takes half of it, (occ + 1) / 2, so consecutive launches run
@@ -580,6 +594,7 @@ void fill_frame_consts(rt::KParams &k)
     f.row_stride = k.row_stride;
     f.tiled_rows = k.tiled_rows;
     f.tiles_x = k.tiles_x;
+    f.tile_lw = k.tile_lw;
     f.n_pixels = k.n_pixels;
     f.sample_begin = k.sample_begin;
     f.div_W = make_udiv(k.W);
@@ -896,9 +911,12 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     if (n_pixels == 0) return RT_OK;
     if (n_pixels >= (1ull << 31)) return fail(RT_ERR_INVALID, "rt_render_device: more than 2^31 pixels in one call");
     k.n_pixels = static_cast<uint32_t>(n_pixels);
-    const bool tiled = (P.width % 8u) == 0u;
-    k.tiles_x = tiled ? P.width / 8u : 1u;
-    k.tiled_rows = tiled ? (k.num_rows / 8u) * 8u : 0u;
+    // 64-pixel tiles (one wave's lanes for one sample), 2^lw wide and 64/2^lw rows tall
+    k.tile_lw = tile_lw_for(P.width, k.row_stride);
+    const uint32_t tw = 1u << k.tile_lw, th = 64u >> k.tile_lw;
+    const bool tiled = (P.width % tw) == 0u;
+    k.tiles_x = tiled ? P.width / tw : 1u;
+    k.tiled_rows = tiled ? (k.num_rows / th) * th : 0u;
     k.n_spheres = sc->n_spheres;
     k.n_materials = sc->n_materials;
 
@@ -1051,6 +1069,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         a.W = P.width;
         a.tiles_x = k.tiles_x;
         a.tiled_rows = k.tiled_rows;
+        a.tile_lw = k.tile_lw;
         a.row_offset = k.row_offset;
         a.row_stride = k.row_stride;
         a.full_frame = k.full_frame;

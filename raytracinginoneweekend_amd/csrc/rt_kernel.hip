@@ -167,8 +167,9 @@ __device__ __forceinline__ void pixel_of(const FC &fc, uint32_t i, uint32_t &x, 
     if (i < tiled_px) {
         uint32_t t = i >> 6, w = i & 63u;
         uint32_t ty = udiv(t, fc.div_tiles_x.m, fc.div_tiles_x.l), tx = t - ty * tiles_x;
-        x = tx * 8u + (w & 7u);
-        rr = ty * 8u + (w >> 3);
+        const uint32_t lw = fc.tile_lw;
+        x = (tx << lw) + (w & ((1u << lw) - 1u));
+        rr = (ty << (6u - lw)) + (w >> lw);
     } else {
         uint32_t j = i - tiled_px;
         rr = udiv(j, fc.div_W.m, fc.div_W.l);
@@ -1505,8 +1506,8 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
         if (i < tiled_px) {
             uint32_t t = i >> 6, w = i & 63u;
             uint32_t ty = t / k.tiles_x, tx = t - ty * k.tiles_x;
-            x = tx * 8u + (w & 7u);
-            rr = ty * 8u + (w >> 3);
+            x = (tx << k.tile_lw) + (w & ((1u << k.tile_lw) - 1u));
+            rr = (ty << (6u - k.tile_lw)) + (w >> k.tile_lw);
         } else {
             uint32_t jj = i - tiled_px;
             rr = jj / k.W;

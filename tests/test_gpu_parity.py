@@ -101,12 +101,19 @@ def test_empty_scene_is_sky():
     assert st.segments == st.primaries  # every primary misses
 
 
-def test_row_partition_invariance_full_frame():
-    """Rows rendered by interleaved 'ranks' and stitched == one full render, bitwise."""
+@pytest.mark.parametrize("tile_lw", ["", "3", "4", "5", "6"])
+@pytest.mark.parametrize("W", [96, 128])
+def test_row_partition_invariance_full_frame(tile_lw, W, monkeypatch):
+    """Rows rendered by interleaved 'ranks' and stitched == one full render, bitwise, whatever
+    the tile shape (RT_TILE_LW; default 8x8; 64x1 falls back to 32x2 at W = 96)."""
     s, m = G.scene("huge")
-    W, H, spp = 96, 50, 4
+    H, spp = 50, 4
+    monkeypatch.setenv("RT_TILE_LW", "3")
+    base, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, full_frame=True))
+    monkeypatch.setenv("RT_TILE_LW", tile_lw)
     whole, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, full_frame=True))
-    for n in (2, 3, 8):
+    _bits_equal(whole, base)
+    for n in (2, 3, 8, 16):
         acc = np.zeros_like(whole)
         for r in range(n):
             part, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, row_offset=r, row_stride=n,

@@ -73,6 +73,10 @@ def parse():
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = leave the environment): "
                          "the library runs one render stream fewer than this, 2..4 (rt_host.cpp pipeline_env)")
+    ap.add_argument("--rehearse-gather", action="store_true",
+                    help="with --rehearse-world N: stand in for rank 0's gather with its device work on the "
+                         "caller stream (the N-1 peer tiles copied into the gather buffer, then the "
+                         "de-interleave copy), to see whether that work waits for CU slots")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_render_c3.json"),
                     help="PMC summary of this kernel (scripts/pmc_round.sh) for roofline.traffic / VALU busy")
     return ap.parse_args()
@@ -182,10 +186,18 @@ def main():
     seg = torch.zeros(3, dtype=torch.int64, device=dev)  # segments, sphere tests, box tests
     stream = torch.cuda.current_stream(dev)
 
+    if rehearse and args.rehearse_gather:
+        fake = torch.empty((rehearse, rows, W, 3), dtype=torch.float32, device=dev)
+        frame_r = torch.empty((rows * rehearse, W, 3), dtype=torch.float32, device=dev)
+
     def step(count_segments):
         ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
         if not rehearse:
             gather(tile)
+        elif args.rehearse_gather:
+            for r in range(1, rehearse):  # one copy kernel per peer, as the gather's receives
+                fake[r].copy_(tile)
+            frame_r.view(rows, rehearse, W, 3).copy_(fake.transpose(0, 1))
 
     for _ in range(args.warmup):
         step(False)
@@ -294,7 +306,9 @@ def main():
                 pmc["valu_insts"] * 2.0 / (1024 * pmc["clock_ghz"] * 1e9 * elapsed / args.steps), 4)
             rec["roofline"]["pmc_source"] = os.path.relpath(args.pmc, REPO)
         if rehearse:
-            rec["rehearsal"] = (f"rank 0 of {rehearse}: rows 0, {rehearse}, ... ({rows} rows), no gather; value = "
+            rec["rehearsal"] = (f"rank 0 of {rehearse}: rows 0, {rehearse}, ... ({rows} rows), "
+                                + ("gather's device copies stood in on the caller stream" if args.rehearse_gather
+                                   else "no gather") + "; value = "
                                 f"this rank's Mrays/s, x{rehearse} for the ideal {rehearse}-GPU job")
         if world == 1 and not args.no_cpu_baseline and not rehearse:
             rec["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], args.camera, args.seed, args.cpu_rows,

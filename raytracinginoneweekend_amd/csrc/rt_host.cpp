@@ -183,6 +183,7 @@ struct rt_scene {
     // queue/segment counters of workspace b not known to be zero (set while a render using
     // them is enqueued, cleared once the accumulation that resets them is enqueued after it)
     bool ctr_dirty[kMaxWs] = {true, true, true, true, true, true, true, true};
+    static_assert(kMaxWs == 8, "ctr_dirty initialiser lists one entry per workspace");
     uint32_t next_buf = 0;  // workspace of the next render pass
     int last_ws = -1;       // workspace of the last render pass issued (its ev_done), -1 = none
     int cu_count = 0;

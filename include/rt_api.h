@@ -182,8 +182,9 @@ int rt_scene_destroy(rt_scene *scene);
 /* Enqueue one render for `stream` (a hipStream_t, or NULL for the null stream).
  * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64[3]
  * that accumulates {segments, sphere tests, cluster box tests} (zero it first). No
- * host sync. The render kernels rotate over 3 internal streams of the scene and 6 slot
- * workspaces, so consecutive frames overlap; they read only the scene and the by-value
+ * host sync. The render kernels rotate over the scene's internal streams (the process's
+ * hardware queues - 1: 3 at HIP's default GPU_MAX_HW_QUEUES=4, at most 4) and 2 slot
+ * workspaces per stream, so consecutive frames overlap; they read only the scene and the by-value
  * arguments, and the writes to d_rgb / d_segments are enqueued on `stream`, so results appear
  * in stream order (RT_PIPELINE=n in the environment sets the streams, 2..4; 0: all on
  * `stream`).                                                                                 */

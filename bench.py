@@ -290,8 +290,8 @@ def main():
             "boxes_per_segment": round(box_tests / max(segments, 1), 2),
         }
         v = {"exact": 0, "scalar": 1, "fast": 2}[args.variant]
-        cull = 0 if args.traversal == "brute" or v == 1 else int(os.environ.get("RT_CULL_STRUCTURE", "7"))
-        kname = f"render_kernel<{v}, {cull}, false, false>"
+        cull = 0 if args.traversal == "brute" or v == 1 else 7
+        kname = f"render_kernel<{v}, {cull}, false>"
         pmc = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
                                             "traversal": args.traversal, "n_gpus": world})
         if pmc and not rehearse:

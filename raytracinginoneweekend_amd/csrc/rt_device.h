@@ -66,12 +66,9 @@ struct KParams {
     const float4 *blob;
     uint32_t blob_units;     // 16-byte units
     uint32_t n_geo, n_always, n_clusters, clus_offset;
-    uint32_t n_clusters_real;  // n_clusters counts never-entered padding boxes (multiple of 4)
     uint32_t n_supers, supers_offset;  // level 2: groups of 4 consecutive clusters, 2 float4 each
     uint32_t use_root;       // level 3: one box over all clusters at supers_offset + 2 n_supers
-    uint32_t cluster_units;  // structure 6: blocks of 8 per cluster = ceil(largest cluster / 8)
-    uint32_t deep_depth;     // > 0: waves 0-2 park paths reaching this many segments for wave 3
-    uint32_t transpose_max;  // structure 7: clusters requested by at most this many lanes (<= 16) run transposed
+    uint32_t transpose_max;  // clusters requested by at most this many lanes (<= 16) are tested transposed
     float clus_pad;          // max over clusters of 1e-3 * (|C|_1 + |e|_1) + 1e-6 (per-ray pad adds 1e-3 |o|_1)
     // shading records in the blob at shade_offset, indexed by original sphere index:
     // {cx, cy, cz, r}, {albedo rgb, param} x n_spheres, then n_spheres kind bytes (16-B padded)

@@ -25,7 +25,7 @@
 
 namespace rt {
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream);
-hipError_t occupancy_render(int variant, int cull, bool deep, int *blocks_per_cu, size_t lds);
+hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream);
 hipError_t occupancy_compat(int *blocks_per_cu);
@@ -166,9 +166,8 @@ struct rt_scene {
     uint32_t blob_units[2] = {0, 0}, n_geo[2] = {0, 0}, n_always[2] = {0, 0}, n_clusters[2] = {0, 0},
              clus_offset[2] = {0, 0};
     float clus_pad[2] = {0.f, 0.f};
-    uint32_t n_clusters_real[2] = {0, 0}, n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
+    uint32_t n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     uint32_t shade_offset[2] = {0, 0};
-    uint32_t cluster_units = 2;  // blocks of 8 in the largest cluster
     // workspaces: consecutive render passes (of one frame or of consecutive frames) rotate over
     // internal streams xs[b] and workspaces slots[b], so a pass renders while the caller stream
     // still accumulates the previous ones
@@ -187,7 +186,7 @@ struct rt_scene {
     uint32_t next_buf = 0;  // workspace of the next render pass
     int last_ws = -1;       // workspace of the last render pass issued (its ev_done), -1 = none
     int cu_count = 0;
-    int occ[4][8][2][2];  // [variant][cull structure 0-7][deep wave][shade records in LDS] blocks per CU, -1 = unknown
+    int occ[4][2][2];  // [variant][culled][shade records in LDS] blocks per CU, -1 = unknown
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
@@ -465,8 +464,8 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
         std::memcpy(&pf, &packed, 4);
         crec.insert(crec.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
     }
-    // 4 never-hitting entries after the last cluster: structure 6 tests members in blocks of
-    // 8 (a cluster of 4 or 12 reads into its successor, harmless for the (t, index) minimum)
+    // 4 never-hitting entries after the last cluster: the transposed member tests read 16
+    // member slots and mask the ones past the cluster's count
     for (int i = 0; i < 4; ++i) {
         geo.insert(geo.end(), {0.f, 0.f, 0.f, -INFINITY});
         sidx.push_back(0xffffffffu);
@@ -603,24 +602,8 @@ void fill_frame_consts(rt::KParams &k)
     f.div_n_pixels = make_udiv(k.n_pixels);
 }
 
-// Culling loop structure (RT_CULL_STRUCTURE selects one for A/B; all give the same bits):
-// 1 = box then its spheres, cluster by cluster; 2 = every box first into per-lane masks,
-// then the wave walks the union of the masks; 3 / 4 = boxes of 2 / 4 clusters at a time
-// (loads batched), then their spheres; 5 = two levels: a box over each 4 clusters, then
-// structure 3 inside the passing ones (config 3 at the time: 8.4 ms; 3: 9.2-9.4; 1: 9.6-9.7);
-// 6 = structure 5's boxes into masks, then member tests compacted over the wave; 7 = structure
-// 5's walk with whole-wave control, a cluster requested by at most RT_TRANSPOSE_MAX lanes tested
-// transposed ((ray, member) pairs over the wave). Default 7 (config 3: 5.03-5.06 ms vs 5.49).
-int cull_structure()
-{
-    const char *e = std::getenv("RT_CULL_STRUCTURE");
-    const int v = e ? std::atoi(e) : 7;
-    static_assert(sizeof(rt_scene::occ[0]) / sizeof(rt_scene::occ[0][0]) == 8, "occupancy cache: structures 0-7");
-    return (v >= 1 && v <= 7) ? v : 7;
-}
-
-// Structure 7: a passing cluster requested by at most RT_TRANSPOSE_MAX lanes (default 16, at
-// most 16) is tested transposed, (ray, member) pairs over the whole wave; same bits either way.
+// A passing cluster requested by at most RT_TRANSPOSE_MAX lanes (default 16, at most 16; 0 =
+// never) is tested transposed, (ray, member) pairs over the whole wave; same bits either way.
 uint32_t transpose_max_env()
 {
     const char *e = std::getenv("RT_TRANSPOSE_MAX");
@@ -678,15 +661,6 @@ uint32_t ws_per_stream_env()
     if (!e || !*e) return 2u;
     const unsigned long v = std::strtoul(e, nullptr, 10);
     return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxWs / kMaxBufs));
-}
-
-// Segments after which waves 0-2 hand a path to the workgroup's deep wave (RT_DEEP_DEPTH;
-// 0 = no deep wave).
-uint32_t deep_depth_env()
-{
-    const char *e = std::getenv("RT_DEEP_DEPTH");
-    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 0ul;
-    return v <= 255 ? static_cast<uint32_t>(v) : 0u;
 }
 
 // RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
@@ -817,7 +791,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         std::memcpy(b.data.data() + at, kinds.data(), kinds.size());
     }
     rt_scene *sc = new rt_scene();
-    for (auto &r : sc->occ) for (auto &x : r) for (auto &y : x) y[0] = y[1] = -1;
+    for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
     sc->device = device;
     sc->n_spheres = n_spheres;
     sc->n_materials = n_materials;
@@ -835,12 +809,10 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         sc->n_clusters[b] = blobs[b].n_clusters;
         sc->clus_offset[b] = blobs[b].clus_offset;
         sc->clus_pad[b] = blobs[b].clus_pad;
-        sc->n_clusters_real[b] = blobs[b].n_clusters_real;
         sc->n_supers[b] = blobs[b].n_supers;
         sc->supers_offset[b] = blobs[b].supers_offset;
         sc->shade_offset[b] = blobs[b].shade_offset;
     }
-    sc->cluster_units = (cluster_max() + 7u) / 8u;
     if (rc == RT_OK) {
         hipError_t e = hipMalloc((void **)&sc->queue_ctr, kCtrWords * sizeof(uint32_t));
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -940,10 +912,7 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         k.dbg = sc->dbg;
     }
     const int b = cull ? 1 : 0;
-    // structures 2 and 6 keep per-lane cluster masks of RT_MAX_CLUSTERS (128) bits; a scene
-    // with more clusters runs structure 5 (any count)
-    int cull_mode = cull ? cull_structure() : 0;
-    if ((cull_mode == 2 || cull_mode == 6) && sc->n_clusters[1] > 128) cull_mode = 5;
+    const int cull_mode = cull ? 7 : 0;
     k.blob = reinterpret_cast<const float4 *>(sc->blob[b]);
     k.blob_units = sc->blob_units[b];
     k.n_geo = sc->n_geo[b];
@@ -951,22 +920,18 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     k.n_clusters = sc->n_clusters[b];
     k.clus_offset = sc->clus_offset[b];
     k.clus_pad = sc->clus_pad[b];
-    k.n_clusters_real = sc->n_clusters_real[b];
     k.n_supers = sc->n_supers[b];
     k.supers_offset = sc->supers_offset[b];
     k.use_root = root_box_env();
-    k.cluster_units = sc->cluster_units;
     k.transpose_max = transpose_max_env();
-    // deep-path wave: structures 0 and 5 (RT_DEEP_DEPTH, 0 = off)
-    k.deep_depth = (cull_mode == 0 || cull_mode == 5) && variant != rt::V_EXACT_SCALAR ? deep_depth_env() : 0u;
     k.shade_offset = sc->shade_offset[b];
     // the shading records (the blob's tail) join the geometry in LDS unless that costs
     // workgroups per CU; RT_SHADE_LDS=0/1 forces the choice for A/B
     auto occ_for = [&](int in_lds, int *out) -> int {
-        int &o = sc->occ[variant][cull_mode][k.deep_depth != 0][in_lds];
+        int &o = sc->occ[variant][cull ? 1 : 0][in_lds];
         if (o < 0) {
             const size_t bytes = variant == rt::V_EXACT_SCALAR ? 0 : static_cast<size_t>(in_lds ? k.blob_units : k.shade_offset) * 16u;
-            RT_HIP(rt::occupancy_render(variant, cull_mode, k.deep_depth != 0, &o, bytes));
+            RT_HIP(rt::occupancy_render(variant, cull_mode, &o, bytes));
             o = std::max(o, 1);
         }
         *out = o;
@@ -1077,12 +1042,8 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
         if (pipe && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
         a.queue_reset = k.queue_ctr;
         a.queue_words = 8 * rt::kQueueStride;
-#ifdef RT_SKIP_ACCUM  // timing-only build: no accumulation (wrong output)
-        (void)a;
-#else
         RT_HIP(rt::launch_accumulate(a, st));
         sc->ctr_dirty[wb] = false;
-#endif
         if (pipe) {
             RT_HIP(hipEventRecord(sc->ev_free[wb], st));
             sc->free_valid[wb] = true;

@@ -56,12 +56,6 @@ __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta)                    
 // ---- RNG: PCG32 XSH-RR per (pixel, sample) stream; the increment is wave-uniform ---------
 __device__ __forceinline__ uint32_t pcg_next(uint64_t &state, uint64_t inc)
 {
-#ifdef RT_RNG_ABLATION  // timing-only build: xorshift32 on the low word (wrong bits by design)
-    uint32_t x = (uint32_t)state | 1u;
-    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
-    state = (state & 0xffffffff00000000ull) | x;
-    return x;
-#endif
     uint64_t old = state;
     state = old * 6364136223846793005ULL + inc;
     uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
@@ -86,20 +80,6 @@ __device__ __forceinline__ float canonical(uint64_t &st, uint64_t inc)
 __device__ __forceinline__ f3 random_in_unit_sphere(uint64_t &st, uint64_t inc)
 {
     f3 p;
-#ifdef RT_REJECT_FIXED  // timing-only build: exactly N attempts, first accepted kept (wrong bits)
-    bool got = false;
-    p = mk(0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < RT_REJECT_FIXED; ++k) {
-        float x = canonical(st, inc) * 2.f + -1.f;
-        float y = canonical(st, inc) * 2.f + -1.f;
-        float z = canonical(st, inc) * 2.f + -1.f;
-        const bool ok = !got && !(x * x + y * y + z * z > 0x1.000002p+0f);
-        p = ok ? mk(x, y, z) : p;
-        got = got || ok;
-    }
-    return p;
-#endif
     do {
         float x = canonical(st, inc) * 2.f + -1.f;
         float y = canonical(st, inc) * 2.f + -1.f;
@@ -230,25 +210,6 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
     for (int w = N / 2; w >= 1; w /= 2)
 #pragma unroll
         for (int k = 0; k < w; ++k) mq[k] = fmaxf(mq[k], mq[k + w]);
-#ifdef RT_DIVERGENT_ROOTS  // A/B build: lane-divergent branches around the root work
-    if (mq[0] > 0.f) {
-        if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
-#pragma unroll
-        for (int k = 0; k < N; ++k) {
-            if (dq[k] > 0.f) {                                               // :62
-                if (STATS) { ++dbg.lane_roots; if (first_active_lane()) ++dbg.wave_roots; }
-                const float q = sqrtf(dq[k]);
-                float t = (-bq[k] - q) / a;                                  // :63
-                if (!(t < RT_TMAX && t > RT_TMIN)) {
-                    t = (-bq[k] + q) / a;                                    // :76
-                    if (!(t < RT_TMAX && t > RT_TMIN)) t = __builtin_nanf("");
-                }
-                const uint32_t id = sidx[i + k];
-                if (t < h.t || (t == h.t && id < h.id)) { h.t = t; h.id = id; }
-            }
-        }
-    }
-#else
     // Wave-uniform branches (ballots) around the root work, lane selects inside: a masked
     // lane costs the same issue slots as a computing one, and uniform branches need no
     // exec-mask save/restore. Lanes without a positive discriminant compute throw-away
@@ -274,18 +235,13 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
             }
         }
     }
-#endif
 }
 
 // Cluster culling: a lane tests a cluster's spheres only if its ray segment (kMIN, t_best]
 // can reach the cluster's AABB grown by a pad that dominates every float error involved
 // (1e-3 x (|o|_1 + max_c(|C|_1 + |e|_1)) against errors below 3e-4 of that),
 // so a culled cluster never holds a sphere whose exact candidate could win: same bits.
-// All boxes of a group of 32 clusters are tested first (straight-line, LDS reads batched)
-// into a per-lane pass mask; the wave walks the union of the masks with a scalar loop and
-// each lane runs a cluster's spheres only if its own bit is set.
 #define RT_PAD_REL 1e-3f
-#define RT_MAX_CLUSTERS 128  // rt_host.cpp sizes clusters so a scene never needs more
 
 // a list of spheres: blocks of 8, then 4, then single spheres (cluster member counts are
 // multiples of 4; the always-tested list has its exact count, e.g. 1 for the ground)
@@ -310,18 +266,6 @@ __device__ __forceinline__ bool box_pass(const RayBox &r, float4 c0, float4 c1, 
     const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
     const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
     return tin <= tout && tout >= t_lo && tin <= t_hi;
-}
-
-// Level 3: one box over every cluster (stored after the level-2 boxes). When no lane's
-// segment reaches it, the wave skips the level-2 loop (returns 0 supers to walk): a ray
-// that misses the padded union box misses every padded box inside it.
-__device__ __forceinline__ uint32_t root_gate(const KParams &p, const RayBox &rb, const float4 *sup, float t_lo,
-                                              float t_hi, uint32_t &tests)
-{
-    if (!p.use_root) return p.n_supers;
-    ++tests;
-    const bool pass = box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, t_hi);
-    return __ballot(pass) ? p.n_supers : 0u;
 }
 
 // Structure 7: the members of a passing cluster, tested transposed. A wave walks the union of
@@ -447,19 +391,11 @@ __device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, co
 template <bool FAST, int CULL, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
-                                           f3 d, Dbg &dbg, uint32_t &tests, uint64_t (&cmask)[2], bool active = true,
-                                           TransposeLds *tw = nullptr)
+                                           f3 d, Dbg &dbg, uint32_t &tests, bool active, TransposeLds *tw)
 {
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
     Hit h{RT_TMAX, 0xffffffffu};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, a, h, dbg);
-#ifdef RT_DUP_ALWAYS  // timing-only build: the always-tested list twice
-    {
-        f3 o2 = o;
-        asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-        run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o2, d, a, h, dbg);
-    }
-#endif
     tests += p.n_always;
     if (CULL) {
         auto safe_rcp = [](float x) {
@@ -470,336 +406,65 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float aix = fabsf(ix), aiy = fabsf(iy), aiz = fabsf(iz);
         const float pad = fmaf(RT_PAD_REL, fabsf(o.x) + fabsf(o.y) + fabsf(o.z), p.clus_pad);
         const float px = pad * aix, py = pad * aiy, pz = pad * aiz;
-        const float tb_hi = h.t * 1.002f;
         const float t_lo = 0.5f * RT_TMIN;
-        if (CULL == 7) {
-            // structure 5's walk with whole-wave control (lanes predicated by `active`), so
-            // that every lane can take part in a cluster's transposed member tests
-            const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
-            const float4 *sup = clus + (p.supers_offset - p.clus_offset);
-            uint32_t n_supers = p.n_supers;
-            if (p.use_root) {
-                tests += active ? 1u : 0u;
-                if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, tb_hi)))
-                    n_supers = 0;
-            }
-            for (uint32_t g = 0; g < n_supers; ++g) {
-                const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
-                tests += active ? 1u : 0u;
-                bool sp = active && box_pass(rb, s0, s1, t_lo, h.t * 1.002f);
-#ifdef RT_DUP_BOXES  // timing-only build: every box test twice (an opaque copy of the ray's constants)
-                {
-                    RayBox r2 = rb;
-                    asm volatile("" : "+v"(r2.ix), "+v"(r2.iy), "+v"(r2.iz), "+v"(r2.px));
-                    sp = sp && box_pass(r2, s0, s1, t_lo, h.t * 1.002f);
-                }
-#endif
-                if (!__ballot(sp)) continue;
-                const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
-                tests += sp ? 4u : 0u;
-                for (uint32_t c = c0i; c < c0i + 4; c += 2) {
-                    const float tb_now = h.t * 1.002f;
-                    const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
-                    bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
-#ifdef RT_DUP_BOXES
-                    {
-                        RayBox r2 = rb;
-                        asm volatile("" : "+v"(r2.ix), "+v"(r2.iy), "+v"(r2.iz), "+v"(r2.px));
-                        pa = pa && box_pass(r2, a0, a1, t_lo, tb_now);
-                        pb = pb && box_pass(r2, b0, b1, t_lo, tb_now);
-                    }
-#endif
-                    cluster_members7<FAST, STATS>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
-                                                  dbg, tests);
-                    cluster_members7<FAST, STATS>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
-                                                  dbg, tests);
-                }
-            }
-            return h;
+        // Two levels under a root box, with whole-wave control (lanes predicated by `active`) so
+        // that every lane can take part in a cluster's transposed member tests: the level-3 box
+        // over every cluster gates the walk (a ray that misses the padded union box misses every
+        // padded box inside it), a level-2 box covers 4 consecutive clusters, and a passing
+        // level-2 box's cluster boxes are tested in pairs against the current t_best.
+        const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
+        const float4 *sup = clus + (p.supers_offset - p.clus_offset);
+        uint32_t n_supers = p.n_supers;
+        if (p.use_root) {
+            tests += active ? 1u : 0u;
+            if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t * 1.002f)))
+                n_supers = 0;
         }
-        if (CULL == 6) {
-            // boxes only: the two-level box walk of structure 5 against the always-list t_best,
-            // into a per-lane mask of passing clusters; the members are tested afterwards by
-            // the whole wave on compacted (ray, cluster half) units (members_compacted)
-            const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
-            const float4 *sup = clus + (p.supers_offset - p.clus_offset);
-            const uint32_t n_supers = root_gate(p, rb, sup, t_lo, tb_hi, tests);
-            for (uint32_t g = 0; g < n_supers; ++g) {
-                const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
-                ++tests;
-                if (!box_pass(rb, s0, s1, t_lo, tb_hi)) continue;
-                const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
-                tests += 4;
-                uint32_t bits = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < 4; ++k)
-                    bits |= box_pass(rb, clus[2 * (c0i + k)], clus[2 * (c0i + k) + 1], t_lo, tb_hi) ? (1u << k) : 0u;
-                const uint64_t sh = (uint64_t)bits << (c0i & 63u);
-                if (c0i < 64u) cmask[0] |= sh;
-                else cmask[1] |= sh;
-            }
-            return h;
-        }
-        if (CULL == 5) {
-            // two levels: a box over each 4 clusters, then pairs of cluster boxes inside
-            const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
-            const float4 *sup = clus + (p.supers_offset - p.clus_offset);
-            const uint32_t n_supers = root_gate(p, rb, sup, t_lo, tb_hi, tests);
-            for (uint32_t g = 0; g < n_supers; ++g) {
-                const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
-                ++tests;
-                if (!box_pass(rb, s0, s1, t_lo, h.t * 1.002f)) continue;
-                const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
-                tests += 4;
-                for (uint32_t c = c0i; c < c0i + 4; c += 2) {
-                    const float tb_now = h.t * 1.002f;
-                    const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
-                    const bool pa = box_pass(rb, a0, a1, t_lo, tb_now), pb = box_pass(rb, b0, b1, t_lo, tb_now);
-                    if (pa) {
-                        const uint32_t scu = __builtin_amdgcn_readfirstlane(__float_as_uint(a1.w));
-                        const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-                        if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
-                        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
-#ifdef RT_DUP_MEMBERS  // timing-only build: each passing cluster's members twice
-                        {
-                            f3 o2 = o;
-                            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-                            run_members<FAST, STATS>(geo, sidx, start, cnt, o2, d, a, h, dbg);
-                        }
-#endif
-                        tests += cnt << 16;
-                    }
-                    if (pb) {
-                        const uint32_t scu = __builtin_amdgcn_readfirstlane(__float_as_uint(b1.w));
-                        const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-                        if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
-                        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
-#ifdef RT_DUP_MEMBERS  // timing-only build: each passing cluster's members twice
-                        {
-                            f3 o2 = o;
-                            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-                            run_members<FAST, STATS>(geo, sidx, start, cnt, o2, d, a, h, dbg);
-                        }
-#endif
-                        tests += cnt << 16;
-                    }
-                }
-            }
-            return h;
-        }
-        if (CULL == 1 || (CULL >= 3 && CULL <= 4)) {
-            // interleaved: boxes of G clusters (G = 1, or 2/4 with their LDS reads issued
-            // together), then each passing cluster's spheres. The box tests of a group use the
-            // t_best from before the group: older, larger, still conservative.
-            constexpr uint32_t G = CULL == 1 ? 1u : (CULL == 3 ? 2u : 4u);
-            for (uint32_t c = 0; c < p.n_clusters; c += G) {
-                bool pass[G];
-                uint32_t sc[G];
+        for (uint32_t g = 0; g < n_supers; ++g) {
+            const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
+            tests += active ? 1u : 0u;
+            const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t * 1.002f);
+            if (!__ballot(sp)) continue;
+            const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
+            tests += sp ? 4u : 0u;
+            for (uint32_t c = c0i; c < c0i + 4; c += 2) {
                 const float tb_now = h.t * 1.002f;
-#pragma unroll
-                for (uint32_t g = 0; g < G; ++g) {
-                    const float4 c0 = clus[2 * (c + g)], c1 = clus[2 * (c + g) + 1];
-                    const float hx = fmaf(c0.w, aix, px), hy = fmaf(c1.x, aiy, py), hz = fmaf(c1.y, aiz, pz);
-                    const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
-                    const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
-                    const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
-                    pass[g] = tin <= tout && tout >= t_lo && tin <= tb_now;
-                    sc[g] = __float_as_uint(c1.w);
-                }
-#pragma unroll
-                for (uint32_t g = 0; g < G; ++g) {
-                    if (pass[g]) {
-                        const uint32_t scu = __builtin_amdgcn_readfirstlane(sc[g]);
-                        const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-                        if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
-                        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
-                        tests += cnt << 16;
-                    }
-                }
-            }
-            tests += p.n_clusters_real;
-            return h;
-        }
-        // pass 1: every box (<= RT_MAX_CLUSTERS), masks per group of 32
-        uint32_t masks[RT_MAX_CLUSTERS / 32], unions[RT_MAX_CLUSTERS / 32];
-#pragma unroll
-        for (uint32_t gi = 0; gi < RT_MAX_CLUSTERS / 32; ++gi) {
-            const uint32_t g = gi * 32;
-            uint32_t mask = 0, any = 0;  // any: wave union, from ballots (active lanes only)
-            if (g < p.n_clusters) {
-                const uint32_t ng = min(32u, p.n_clusters - g);
-
-#pragma unroll 1
-                for (uint32_t c = 0; c < ng; ++c) {
-                    const float4 c0 = clus[2 * (g + c)], c1 = clus[2 * (g + c) + 1];  // {C, ex}, {ey, ez, -, start|count}
-                    const float hx = fmaf(c0.w, aix, px), hy = fmaf(c1.x, aiy, py), hz = fmaf(c1.y, aiz, pz);
-                    const float tcx = fmaf(c0.x, ix, -oix), tcy = fmaf(c0.y, iy, -oiy), tcz = fmaf(c0.z, iz, -oiz);
-                    const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
-                    const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
-                    const bool pass = tin <= tout && tout >= t_lo && tin <= tb_hi;
-                    mask |= pass ? (1u << c) : 0u;
-                    any |= __ballot(pass) ? (1u << c) : 0u;
-                }
-            }
-            masks[gi] = mask;
-            unions[gi] = any;
-        }
-        tests += p.n_clusters_real;
-        // pass 2: the wave walks the union of the lanes' masks
-#pragma unroll
-        for (uint32_t gi = 0; gi < RT_MAX_CLUSTERS / 32; ++gi) {
-            const uint32_t g = gi * 32;
-            if (g >= p.n_clusters) break;
-            const uint32_t mask = masks[gi];
-            uint32_t u = __builtin_amdgcn_readfirstlane(unions[gi]);
-            while (u) {
-                const uint32_t c = __builtin_ctz(u);
-                u &= u - 1u;
-                if (mask & (1u << c)) {
-                    const uint32_t sc = __float_as_uint(clus[2 * (g + c) + 1].w);
-                    const uint32_t start = __builtin_amdgcn_readfirstlane(sc & 0xffffu);
-                    const uint32_t cnt = __builtin_amdgcn_readfirstlane(sc >> 16);
-                    run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
-                    tests += cnt << 16;
-                }
+                const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
+                const bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
+                cluster_members7<FAST, STATS>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
+                                              dbg, tests);
+                cluster_members7<FAST, STATS>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
+                                              dbg, tests);
             }
         }
     }
     return h;
 }
 
-// Structure 6, phase B: the member tests of every (lane, passing cluster) pair of the wave,
-// compacted. A pair is split into units of 8 member slots (cluster_units per cluster); the
-// units are numbered by an exclusive prefix over the lanes (bit-plane ballots), dealt 64 per
-// round to ALL lanes of the wave (idle lanes included), and each unit's best candidate is
-// folded into its owner's LDS key with one ds_min_u64: key = bits(t) << 32 | original index,
-// and for t > 0 the u64 order IS the (t, index) lexicographic order of closest_hit, so the
-// result is the same whatever lane tests what, in whatever order. A half-block reading past
-// its cluster tests the next cluster's spheres (or never-hitting padding): extra genuine
-// candidates never change the minimum. Must be called by the whole wave (uniform control).
-template <bool FAST, bool STATS>
-__device__ __forceinline__ void members_compacted(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
-                                                  const float4 *__restrict__ clus, uint64_t *wkey, uint32_t *wlist,
-                                                  const uint64_t (&cmask)[2], f3 o, f3 d, Hit &h, Dbg &dbg,
-                                                  uint32_t &tests, uint32_t p_units)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t k = (uint32_t)(__popcll(cmask[0]) + __popcll(cmask[1]));  // passing clusters
-    // exclusive prefix E of k over the lanes, and the wave total T
-    uint32_t E = 0, T = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 8; ++b) {
-        const uint64_t bb = __ballot((k >> b) & 1u);
-        E += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
-        T += (uint32_t)__popcll(bb) << b;
-    }
-    T = __builtin_amdgcn_readfirstlane(T);
-    if (T == 0) return;
-    if (k) wkey[lane] = ((uint64_t)__float_as_uint(h.t) << 32) | h.id;
-    const uint32_t U = p_units;  // blocks of 8 per cluster (cluster size / 8, rounded up)
-    const uint32_t units = U * T;
-    for (uint32_t base = 0; base < units; base += 64u) {
-        // emission: each owner writes its units in [base, base + 64)
-        if (k) {
-            uint32_t j = 0;
-#pragma unroll
-            for (int w = 0; w < 2; ++w) {
-                uint64_t m = cmask[w];
-                while (m) {
-                    const uint32_t c = (uint32_t)__builtin_ctzll(m) + 64u * (uint32_t)w;
-                    m &= m - 1u;
-                    const uint32_t u0 = U * (E + j++);
-                    if (u0 + U > base && u0 < base + 64u) {
-                        const uint32_t e = lane | (c << 6);
-                        for (uint32_t hb = 0; hb < U; ++hb)
-                            if (u0 + hb >= base && u0 + hb < base + 64u) wlist[u0 + hb - base] = e | (hb << 13);
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t n_here = min(64u, units - base);
-        const uint32_t e = lane < n_here ? wlist[lane] : 0u;
-        const uint32_t owner = e & 63u;
-        // the owner's ray, read across lanes (every lane active here)
-        const f3 ro = mk(__shfl(o.x, owner), __shfl(o.y, owner), __shfl(o.z, owner));
-        const f3 rd = mk(__shfl(d.x, owner), __shfl(d.y, owner), __shfl(d.z, owner));
-        if (lane < n_here) {
-            const uint32_t c = (e >> 6) & 127u, half = e >> 13;  // half: the unit's block of 8
-            const uint32_t sc = __float_as_uint(clus[2 * c + 1].w);
-            const uint32_t start = sc & 0xffffu, cnt = sc >> 16;
-            if (8u * half < cnt) {
-                const float a = rd.x * rd.x + rd.y * rd.y + rd.z * rd.z;
-                Hit u{RT_TMAX, 0xffffffffu};
-                test_block8<FAST, STATS>(geo, sidx, start + 8u * half, ro, rd, a, u, dbg);
-                tests += 8u << 16;
-                if (u.id != 0xffffffffu)
-                    atomicMin((unsigned long long *)(wkey + owner), ((uint64_t)__float_as_uint(u.t) << 32) | u.id);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (k) {
-        const uint64_t key = wkey[lane];
-        h.t = __uint_as_float((uint32_t)(key >> 32));
-        h.id = (uint32_t)key;
-    }
-}
-
 // ---- the megakernel ----------------------------------------------------------------------
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
 #endif
-// ---- deep paths: one wave per workgroup takes them over --------------------------------
-// 0.18% of config 3's samples never leave the glass sphere and run to max_depth; those and
-// other deep paths are 10% of the segments but, spread over every wave, make almost every
-// wave iteration pay for their dielectric shading and cluster members. With DEEP, waves 0-2 of
-// a workgroup park a path that is about to trace segment p.deep_depth + 1 in a workgroup LDS
-// queue (when it has room) and refill the lane; wave 3 takes parked paths before new items,
-// so deep paths share waves with each other. The result is unchanged: a path's state moves
-// whole, and every sample still lands in its own slot.
-constexpr uint32_t kDeepQ = 64;
-struct DeepQueue {
-    uint32_t head, tail, producers, pad;  // head: claimed by producers; tail: consumed by wave 3
-    uint32_t gen[kDeepQ];                 // slot generation (pos / kDeepQ + 1) once written
-    uint4 st[kDeepQ][5];                  // bits of o, d, att, {rng lo, rng hi, pix, ls}, pn
-    uint32_t meta[kDeepQ];                // depth | pend << 8 | pend_metal << 9
-};
-
 // Structure 7 (the default) is held to 6 waves per SIMD: unhinted it takes 83 VGPRs (5 waves);
 // hinted, the allocator keeps 79 and parks one 12-byte constant that only the metal-absorption
 // path reloads (measured: 5.03-5.06 ms vs 5.19-5.24 per config-3 launch).
-template <int V, int CULL, bool STATS, bool DEEP>
-constexpr int kMinWaves = (CULL == 7 && !STATS && !DEEP) ? 6 : RT_MIN_WAVES_PER_SIMD;
-template <int V, int CULL, bool STATS, bool DEEP>
-__global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render_kernel(const KParams p)
+template <int V, int CULL, bool STATS>
+constexpr int kMinWaves = (CULL == 7 && !STATS) ? 6 : RT_MIN_WAVES_PER_SIMD;
+template <int V, int CULL, bool STATS>
+__global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kernel(const KParams p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
     // Scene blob -> LDS (or read in place from global for the scalar-cache A/B variant):
     // [geo float4 x n_geo][sidx u32 x n_geo, 16-B padded][clusters float4 x 2 x n_clusters]
     extern __shared__ float4 lds_blob[];
     const float4 *blob;
-    DeepQueue *dq = nullptr;
-    if constexpr (DEEP) {
-        __shared__ DeepQueue s_dq;
-        dq = &s_dq;
-        if (threadIdx.x < kDeepQ) dq->gen[threadIdx.x] = 0u;
-        if (threadIdx.x == 0) { dq->head = 0u; dq->tail = 0u; dq->producers = 3u; }
-    }
     if constexpr (V == V_EXACT_SCALAR) {
         blob = p.blob;
-        if (DEEP) __syncthreads();
     } else {
         for (uint32_t i = threadIdx.x; i < p.lds_units; i += blockDim.x) lds_blob[i] = p.blob[i];
         __syncthreads();
         blob = lds_blob;
     }
-    const bool deep_wave = DEEP && (threadIdx.x >> 6) == 3u;  // the consumer of parked paths
-    uint32_t qtail = 0;                                        // deep wave: its copy of dq->tail
     // Per-render constants used only where a sample or an item starts are re-read from the
     // kernarg segment at each use (scalar loads) through a pointer made opaque every loop
     // iteration, so they do not pin ~30 SGPRs for the whole kernel (SGPR count bounds the
@@ -813,19 +478,11 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
     const float4 *clus = blob + p.clus_offset;
 
     const uint32_t lane = threadIdx.x & 63u;
-    // structure 6: per-wave LDS scratch of the compacted member tests (owner keys, unit list)
-    uint64_t *wkey = nullptr;
-    uint32_t *wlist = nullptr;
+    // per-wave LDS of the transposed member tests
     TransposeLds *tw = nullptr;
     if constexpr (CULL == 7) {
         __shared__ TransposeLds s_tw[4];
         tw = &s_tw[threadIdx.x >> 6];
-    }
-    if constexpr (CULL == 6) {
-        __shared__ uint64_t s_wkey[4][64];
-        __shared__ uint32_t s_wlist[4][64];
-        wkey = s_wkey[threadIdx.x >> 6];
-        wlist = s_wlist[threadIdx.x >> 6];
     }
 
     // wave-uniform cursor over the item space
@@ -869,40 +526,6 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
         // ---- refill items for idle lanes and start their samples -------------------
         uint64_t need = __ballot(!alive);
         bool fresh = false;
-        if (DEEP && deep_wave && need) {
-            // parked paths first, in queue order; a slot is read once its producer has
-            // published it (generation), and tail moves only after the reads
-            const uint32_t h = __builtin_amdgcn_readfirstlane(__atomic_load_n(&dq->head, __ATOMIC_ACQUIRE));
-            const uint32_t k = min((uint32_t)__popcll(need), h - qtail);
-            if (k) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                if (!alive && rank < k) {
-                    const uint32_t pos = qtail + rank, sl = pos % kDeepQ;
-                    while (__atomic_load_n(&dq->gen[sl], __ATOMIC_ACQUIRE) != pos / kDeepQ + 1u)
-                        __builtin_amdgcn_s_sleep(1);
-                    const uint4 a0 = dq->st[sl][0], a1 = dq->st[sl][1], a2 = dq->st[sl][2], a3 = dq->st[sl][3];
-                    const uint4 a4 = dq->st[sl][4];
-                    const uint32_t mt = dq->meta[sl];
-                    o = mk(__uint_as_float(a0.x), __uint_as_float(a0.y), __uint_as_float(a0.z));
-                    d = mk(__uint_as_float(a1.x), __uint_as_float(a1.y), __uint_as_float(a1.z));
-                    att = mk(__uint_as_float(a2.x), __uint_as_float(a2.y), __uint_as_float(a2.z));
-                    pn = make_float4(__uint_as_float(a4.x), __uint_as_float(a4.y), __uint_as_float(a4.z),
-                                     __uint_as_float(a4.w));
-                    rng = ((uint64_t)a3.y << 32) | a3.x;
-                    pix = a3.z;
-                    ls = a3.w;
-                    depth = mt & 0xffu;
-                    pend = (mt >> 8) & 1u;
-                    pend_metal = (mt >> 9) & 1u;
-                    alive = true;
-                }
-                qtail += k;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0) __atomic_store_n(&dq->tail, qtail, __ATOMIC_RELEASE);
-                need = __ballot(!alive);
-            }
-        }
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
             if (cnext >= cend) {
@@ -1006,15 +629,6 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
                 rc = ((uint64_t)__float_as_uint(o.y) << 32) | __float_as_uint(o.x);
             }
             uint64_t st = lens ? rc : rng;
-#ifdef RT_DUP_REJECT  // timing-only build: the rejection loop twice (the copy is discarded)
-            {
-                uint64_t st2 = st;
-                asm volatile("" : "+v"(st2));
-                const f3 r2 = random_in_unit_sphere(st2, inc);
-                float sink = r2.x + r2.y + r2.z;
-                asm volatile("" ::"v"(sink));
-            }
-#endif
             bool got;
             const f3 r = random_in_unit_sphere_capped(st, inc, got);
             if (!got) {
@@ -1058,15 +672,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
             }
         }
         stamp(1);
-        if (__ballot(alive) == 0) {  // only when the item space is exhausted
-            if (!DEEP || !deep_wave) break;
-            // the deep wave leaves once no producer is left and the queue is empty
-            const uint32_t h = __builtin_amdgcn_readfirstlane(__atomic_load_n(&dq->head, __ATOMIC_ACQUIRE));
-            const uint32_t pr = __builtin_amdgcn_readfirstlane(__atomic_load_n(&dq->producers, __ATOMIC_ACQUIRE));
-            if (pr == 0u && h == qtail) break;
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
+        if (__ballot(alive) == 0) break;  // only when the item space is exhausted
         if (STATS && lane == 0) {
             ++dbg_iters;
             if (exhausted) {
@@ -1078,29 +684,16 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && !defer && depth < p.max_depth;  // depth check: main.cxx:74
         Hit h{RT_TMAX, 0xffffffffu};
-        uint64_t cmask[2] = {0, 0};
         uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
-            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, cmask, seg, tw);
+            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, seg, tw);
             if (!seg) {
                 h = Hit{RT_TMAX, 0xffffffffu};
                 tally = 0;
             }
         } else if (seg) {
-            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, cmask);
+            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, true, nullptr);
         }
-#ifdef RT_DUP_HIT  // timing-only build: the closest-hit search twice on an opaque copy of the ray
-        if (seg) {
-            f3 o2 = o;
-            asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
-            uint32_t t2 = 0;
-            uint64_t cm2[2] = {0, 0};
-            const Hit h2 = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o2, d, dbg, t2, cm2);
-            if (h2.t < h.t) h = h2;
-        }
-#endif
-        if constexpr (CULL == 6)
-            members_compacted<FAST, STATS>(geo, sidx, clus, wkey, wlist, cmask, o, d, h, dbg, tally, p.cluster_units);
         stamp(2);
         {
             const uint32_t al = seg ? p.n_always : 0u;
@@ -1164,22 +757,6 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
                             pend = true;
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
-#ifdef RT_DUP_DIEL  // timing-only build: the dielectric shading twice on an opaque copy (result discarded)
-                            {
-                                f3 u2 = ud;
-                                asm volatile("" : "+v"(u2.x), "+v"(u2.y), "+v"(u2.z));
-                                f3 ow2 = mk(-hn.x, -hn.y, -hn.z);
-                                float ri2 = md.w, c2 = dot(u2, hn);
-                                if (c2 <= 0.f) { ow2 = ow2 * -1.f; ri2 = 1.f / ri2; c2 *= -1.f; }
-                                const f3 rr2 = refract(u2, ow2, ri2);
-                                float pr2 = 1.f;
-                                if (rr2.x * rr2.x + rr2.y * rr2.y + rr2.z * rr2.z > 0.f) pr2 = schlick(ri2, c2);
-                                uint64_t st2 = rng;
-                                asm volatile("" : "+v"(st2));
-                                const float sink = canonical(st2, inc_data) < pr2 ? rr2.x : rr2.y;
-                                asm volatile("" ::"v"(sink));
-                            }
-#endif
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w;
                             float cosv = dot(ud, hn);
@@ -1208,47 +785,6 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS, DEEP>)) void render
                 dst[2] = col.z;
             }
         }
-        if constexpr (DEEP) {
-            // waves 0-2: park paths that reach p.deep_depth segments (room permitting)
-            const uint64_t pm = deep_wave ? 0ull : __ballot(alive && depth >= p.deep_depth);
-            if (pm) {
-                const uint32_t n = (uint32_t)__popcll(pm);
-                uint32_t h0 = 0, n2 = 0;
-                if (lane == __builtin_ctzll(pm)) {
-                    for (;;) {
-                        const uint32_t h = __atomic_load_n(&dq->head, __ATOMIC_RELAXED);
-                        const uint32_t t = __atomic_load_n(&dq->tail, __ATOMIC_ACQUIRE);
-                        n2 = min(n, kDeepQ - (h - t));
-                        h0 = h;
-                        if (n2 == 0u) break;
-                        uint32_t expect = h;
-                        if (__atomic_compare_exchange_n(&dq->head, &expect, h + n2, false, __ATOMIC_ACQ_REL,
-                                                        __ATOMIC_RELAXED))
-                            break;
-                    }
-                }
-                h0 = __builtin_amdgcn_readlane(h0, __builtin_ctzll(pm));
-                n2 = __builtin_amdgcn_readlane(n2, __builtin_ctzll(pm));
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
-                if ((pm >> lane) & 1ull && rank < n2) {
-                    const uint32_t pos = h0 + rank, sl = pos % kDeepQ;
-                    dq->st[sl][0] = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), 0u);
-                    dq->st[sl][1] = make_uint4(__float_as_uint(d.x), __float_as_uint(d.y), __float_as_uint(d.z), 0u);
-                    dq->st[sl][2] = make_uint4(__float_as_uint(att.x), __float_as_uint(att.y), __float_as_uint(att.z), 0u);
-                    dq->st[sl][3] = make_uint4((uint32_t)rng, (uint32_t)(rng >> 32), pix, ls);
-                    dq->st[sl][4] = make_uint4(__float_as_uint(pn.x), __float_as_uint(pn.y), __float_as_uint(pn.z),
-                                               __float_as_uint(pn.w));
-                    dq->meta[sl] = depth | ((uint32_t)pend << 8) | ((uint32_t)pend_metal << 9);
-                    __atomic_store_n(&dq->gen[sl], pos / kDeepQ + 1u, __ATOMIC_RELEASE);
-                    alive = false;
-                    pend = false;  // the pending scatter left with the path
-                }
-            }
-        }
-    }
-    if constexpr (DEEP) {
-        if (!deep_wave && lane == 0) __atomic_fetch_sub(&dq->producers, 1u, __ATOMIC_RELEASE);
     }
 
     if (p.segments) {
@@ -1537,45 +1073,37 @@ __global__ __launch_bounds__(256) void epilogue_rgb8_kernel(const float *in, uin
 }
 
 // ---- launchers (called from rt_host.cpp) ---------------------------------------------
-template <int V, bool STATS> static const void *ptr3(int cull, bool deep)
+// cull: 0 = brute force (every sphere, index order), 7 = two-level cluster walk with
+// transposed member tests (the default)
+template <int V, bool STATS> static const void *ptr_cull(int cull)
 {
-    if (deep && cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS, true>);
-    if (deep && cull == 0) return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, true>);
-    if (deep) return nullptr;
-    if (cull == 1) return reinterpret_cast<const void *>(&render_kernel<V, 1, STATS, false>);
-    if (cull == 2) return reinterpret_cast<const void *>(&render_kernel<V, 2, STATS, false>);
-    if (cull == 3) return reinterpret_cast<const void *>(&render_kernel<V, 3, STATS, false>);
-    if (cull == 4) return reinterpret_cast<const void *>(&render_kernel<V, 4, STATS, false>);
-    if (cull == 5) return reinterpret_cast<const void *>(&render_kernel<V, 5, STATS, false>);
-    if (cull == 6) return reinterpret_cast<const void *>(&render_kernel<V, 6, STATS, false>);
-    if (cull == 7) return reinterpret_cast<const void *>(&render_kernel<V, 7, STATS, false>);
-    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, false>);
+    if (cull == 7) return reinterpret_cast<const void *>(&render_kernel<V, 7, STATS>);
+    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS>);
 }
 
-static const void *render_ptr(int variant, int cull, bool deep)
+static const void *render_ptr(int variant, int cull)
 {
     switch (variant) {
-    case V_EXACT_LDS: return ptr3<V_EXACT_LDS, false>(cull, deep);
-    case V_FAST_LDS: return ptr3<V_FAST_LDS, false>(cull, deep);
-    case V_EXACT_SCALAR:
-        return cull || deep ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false, false>);
-    case V_STATS_LDS: return ptr3<V_EXACT_LDS, true>(cull, deep);
+    case V_EXACT_LDS: return ptr_cull<V_EXACT_LDS, false>(cull);
+    case V_FAST_LDS: return ptr_cull<V_FAST_LDS, false>(cull);
+    case V_EXACT_SCALAR: return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false>);
+    case V_STATS_LDS: return ptr_cull<V_EXACT_LDS, true>(cull);
     default: return nullptr;
     }
 }
 
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream)
 {
-    const void *fn = render_ptr(variant, cull, p.deep_depth != 0);
+    const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;
     const size_t lds = (size_t)p.lds_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};
     return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, stream);
 }
 
-hipError_t occupancy_render(int variant, int cull, bool deep, int *blocks_per_cu, size_t lds)
+hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds)
 {
-    const void *fn = render_ptr(variant, cull, deep);
+    const void *fn = render_ptr(variant, cull);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
 }

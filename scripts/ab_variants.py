@@ -32,22 +32,18 @@ ds = rt.DeviceScene(arrays)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
-# kind:traversal[:cN][:LN][:tN] -- traversal "cullN" sets RT_CULL_STRUCTURE=N, "cN" RT_CHUNK_ITEMS=N,
-# "L0"/"L1" RT_SHADE_LDS, "tN" RT_TAIL_PCT=N, "r0"/"r1" RT_ROOT_BOX, "s0" no counters, "DN" RT_DEEP_DEPTH=N,
-# "xN" RT_TRANSPOSE_MAX=N (structure 7)
+# kind:traversal[:cN][:LN][:tN] -- "cN" RT_CHUNK_ITEMS=N, "L0"/"L1" RT_SHADE_LDS, "tN" RT_TAIL_PCT=N,
+# "r0"/"r1" RT_ROOT_BOX, "s0" no counters, "xN" RT_TRANSPOSE_MAX=N
 variants = [(v.split(":")[0], v.split(":")[1], v.split(":")[2:]) for v in a.variants.split(",")]
 times = {":".join([k, t] + x): [] for k, t, x in variants}
 ref = None
 segs = {}
 for r in range(a.rounds + 1):
     for kind, trav, extra in variants:
-        if trav.startswith("cull") and len(trav) > 4:
-            os.environ["RT_CULL_STRUCTURE"] = trav[4:]
         os.environ["RT_CHUNK_ITEMS"] = "".join(x[1:] for x in extra if x.startswith("c"))
         os.environ["RT_SHADE_LDS"] = "".join(x[1:] for x in extra if x.startswith("L"))
         os.environ["RT_TAIL_PCT"] = "".join(x[1:] for x in extra if x.startswith("t"))
         os.environ["RT_ROOT_BOX"] = "".join(x[1:] for x in extra if x.startswith("r"))
-        os.environ["RT_DEEP_DEPTH"] = "".join(x[1:] for x in extra if x.startswith("D"))
         os.environ["RT_TRANSPOSE_MAX"] = "".join(x[1:] for x in extra if x.startswith("x"))
         p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
                            brute_force=trav == "brute")

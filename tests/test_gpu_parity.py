@@ -17,7 +17,9 @@ from raytracinginoneweekend_amd import _abi as abi
 pytestmark = pytest.mark.gpu
 
 RENDERS = sorted(n for n, m in G.manifest()["renders"].items() if m["rng"] == "pcg")
-VARIANTS = {"clustered": {}, "clustered2": {"_structure": "2"}, "clustered5": {"_structure": "5"}, "brute": {"brute_force": True},
+# clustered0: the same two-level walk with every cluster's members tested per lane (never
+# transposed, RT_TRANSPOSE_MAX=0)
+VARIANTS = {"clustered": {}, "clustered0": {"_transpose": "0"}, "brute": {"brute_force": True},
             "scalar": {"scalar_scene": True}}
 
 
@@ -49,8 +51,8 @@ def test_golden_render_f32(name, variant, monkeypatch):
     scene = G.scene(meta["scene"])
     cam = rt.Camera.default(meta["width"], meta["height"], G.camera_mode(meta))
     kw = dict(VARIANTS[variant])
-    if "_structure" in kw:
-        monkeypatch.setenv("RT_CULL_STRUCTURE", kw.pop("_structure"))
+    if "_transpose" in kw:
+        monkeypatch.setenv("RT_TRANSPOSE_MAX", kw.pop("_transpose"))
     img, st = rt.render_f32(scene, _params(meta, **kw), cam)
     _bits_equal(img, f32)
     assert st.primaries == meta["width"] * meta["num_rows"] * meta["spp"]
@@ -196,9 +198,9 @@ def _random_scene(rng, n, spread, center=(0.0, 0.0, 0.0)):
     (3, 400, 3.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
     (4, 800, 5.0, (200.0, 0.0, -150.0), abi.RT_CAMERA_CORRECTED),
 ])
-@pytest.mark.parametrize("structure", ["1", "2", "3", "4", "5", "6", "7"])
-def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, structure, monkeypatch):
-    monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
+@pytest.mark.parametrize("transpose", ["0", "4", "16"])
+def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, transpose, monkeypatch):
+    monkeypatch.setenv("RT_TRANSPOSE_MAX", transpose)
     rng = np.random.default_rng(seed)
     s, m = _random_scene(rng, n, spread, center)
     W, H, spp = 48, 32, 4
@@ -370,13 +372,12 @@ def test_cuda_impl_replacement_u8():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cluster_size", ["4", "8", "12", "24", "32", "64"])
-@pytest.mark.parametrize("structure", ["5", "6", "7"])
-def test_cluster_size_bit_exact(cluster_size, structure, monkeypatch):
-    """Any cluster size (RT_CLUSTER_SIZE, read when the scene is created) and loop structure
-    gives the oracle's bits: structure 6 deals ceil(size / 8) units of 8 members per
-    (lane, cluster) pair."""
+@pytest.mark.parametrize("transpose", ["0", "16"])
+def test_cluster_size_bit_exact(cluster_size, transpose, monkeypatch):
+    """Any cluster size (RT_CLUSTER_SIZE, read when the scene is created) gives the oracle's
+    bits, with members tested per lane or transposed (clusters above 16 members always per lane)."""
     monkeypatch.setenv("RT_CLUSTER_SIZE", cluster_size)
-    monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
+    monkeypatch.setenv("RT_TRANSPOSE_MAX", transpose)
     rng = np.random.default_rng(11)
     for s, m in (G.scene("huge"), _random_scene(rng, 900, 10.0)):
         W, H, spp = 40, 24, 4
@@ -389,11 +390,10 @@ def test_cluster_size_bit_exact(cluster_size, structure, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("structure", ["2", "5", "6", "7"])
-def test_many_clusters_bit_exact(structure, monkeypatch):
-    """A scene with more than 128 clusters (5000 spheres): structures 2 and 6, whose per-lane
-    masks hold 128 clusters, fall back to structure 5; every structure gives the oracle's bits."""
-    monkeypatch.setenv("RT_CULL_STRUCTURE", structure)
+@pytest.mark.parametrize("transpose", ["0", "16"])
+def test_many_clusters_bit_exact(transpose, monkeypatch):
+    """A scene with more than 128 clusters (5000 spheres) gives the oracle's bits."""
+    monkeypatch.setenv("RT_TRANSPOSE_MAX", transpose)
     rng = np.random.default_rng(5)
     s, m = _random_scene(rng, 5000, 40.0)
     W, H, spp = 32, 24, 2
@@ -403,28 +403,6 @@ def test_many_clusters_bit_exact(structure, monkeypatch):
     want, seg = O.render_f32(s, m, cam, p)
     _bits_equal(got, want)
     assert st.segments == seg
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("deep,brute,budget_samples", [("1", False, 0), ("2", False, 0), ("2", True, 0),
-                                                        ("8", False, 0), ("2", False, 4), ("3", True, 8)])
-def test_deep_wave_bit_exact(deep, brute, budget_samples, monkeypatch):
-    """RT_DEEP_DEPTH: waves 0-2 of a workgroup hand paths that reach `deep` segments to wave 3
-    through an LDS queue (whole path state, pending scatter included); the oracle's bits and
-    segment count for the huge scene (glass-sphere paths run to max_depth) with culling or
-    brute force, in one pass or several."""
-    monkeypatch.setenv("RT_DEEP_DEPTH", deep)
-    if budget_samples:
-        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(96 * 40 * 12 * budget_samples))
-    s, m = G.scene("huge")
-    W, H, spp = 96, 40, 9
-    for mode in (abi.RT_CAMERA_REFERENCE, abi.RT_CAMERA_CORRECTED):
-        cam = O.camera_default(W, H, mode)
-        p = rt.make_params(W, H, spp, 64, 13, brute_force=brute)
-        got, st = rt.render_f32((s, m), p, cam)
-        want, seg = O.render_f32(s, m, cam, p)
-        _bits_equal(got, want)
-        assert st.segments == seg
 
 
 @pytest.mark.gpu

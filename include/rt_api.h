@@ -18,7 +18,8 @@
  * (src/CUDA/cuda_impl.cu) are selected with RT_FLAG_CUDA_COMPAT or rt_render_cuda_impl.
  *
  * Threading: every call is synchronous unless its name ends in _device; calls on one
- * rt_scene come from one host thread. Errors: a negative status; rt_last_error() returns a
+ * rt_scene come from one host thread. Device calls on one rt_scene may use different
+ * streams: a call on a new stream is ordered after the previous call's work. Errors: a negative status; rt_last_error() returns a
  * thread-local message for the last failing call on this thread.
  */
 #ifndef RT_API_H
@@ -40,7 +41,8 @@ enum rt_status {
     RT_ERR_DEVICE = -2,      /* HIP runtime error (no device, launch/alloc failure)     */
     RT_ERR_CAPACITY = -3,    /* caller buffer too small                                 */
     RT_ERR_UNSUPPORTED = -4, /* feature not available in this build / on this host     */
-    RT_ERR_COMM = -5         /* RCCL failure in the multi-GPU path                      */
+    RT_ERR_COMM = -5,        /* RCCL failure in the multi-GPU path                      */
+    RT_ERR_IO = -6           /* file could not be opened or written (rt_write_ppm)       */
 };
 
 /* ---- scene records ----------------------------------------------------------------
@@ -157,11 +159,23 @@ int rt_render_rgb8(const rt_sphere *spheres, uint32_t n_spheres,
                    uint8_t *rgb_out, rt_stats *stats);
 /* Row-interleaved split over ngpu devices of this process (device i renders rows
  * y ≡ i mod ngpu), gathered to device 0 with RCCL over xGMI, then copied to rgb_out
- * (full frame, height*width*3 floats). ngpu <= 0 uses every visible device.            */
+ * (full frame, height*width*3 floats). ngpu <= 0 uses every visible device. One-shot:
+ * builds and tears down an rt_multi context (below) around the frame.                 */
 int rt_render_multi_f32(const rt_sphere *spheres, uint32_t n_spheres,
                         const rt_material *materials, uint32_t n_materials,
                         const rt_camera *camera, const rt_params *params, int ngpu,
                         float *rgb_out, rt_stats *stats);
+/* The same with the gamma/u8 epilogue (src/main.cxx:39-45,77-85) run on every rank's tile
+ * before the gather: 3 bytes per pixel cross xGMI instead of 12 (height*width*3 bytes).  */
+int rt_render_multi_rgb8(const rt_sphere *spheres, uint32_t n_spheres,
+                         const rt_material *materials, uint32_t n_materials,
+                         const rt_camera *camera, const rt_params *params, int ngpu,
+                         uint8_t *rgb_out, rt_stats *stats);
+
+/* app::save_to_file (src/main.cxx:87-101): binary PPM "P6\n<width> <height>\n255\n"
+ * followed by width*height RGB texels, row 0 first. RT_ERR_IO if the file cannot be
+ * written (the reference throws "bad file").                                           */
+int rt_write_ppm(const char *path, const uint8_t *rgb, uint32_t width, uint32_t height);
 
 /* The literal replacement of the reference's accelerated entry point
  *     void cuda_impl(uint32_t width, uint32_t height, std::vector<u8vec3> &image_texels)
@@ -182,7 +196,8 @@ int rt_scene_destroy(rt_scene *scene);
 /* Enqueue one render for `stream` (a hipStream_t, or NULL for the null stream).
  * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64[3]
  * that accumulates {segments, sphere tests, cluster box tests} (zero it first). No
- * host sync. The render kernels rotate over the scene's internal streams (the process's
+ * host sync (a call whose slot workspace or accumulation buffer must grow synchronises the
+ * device once, before enqueuing). The render kernels rotate over the scene's internal streams (the process's
  * hardware queues - 1: 3 at HIP's default GPU_MAX_HW_QUEUES=4, at most 4) and 2 slot
  * workspaces per stream, so consecutive frames overlap; they read only the scene and the by-value
  * arguments, and the writes to d_rgb / d_segments are enqueued on `stream`, so results appear
@@ -190,10 +205,12 @@ int rt_scene_destroy(rt_scene *scene);
  * `stream`).                                                                                 */
 int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
                      float *d_rgb, void *stream, uint64_t *d_segments);
-/* Durations (ms, HIP events on the render kernels' stream) of the render kernel launches of the
- * most recent calls of rt_render_device on this scene, oldest first: entry i is the sum
- * over the passes of one call. Writes up to `max` entries, *n = entries written. Waits for
- * those calls to finish.                                                                */
+/* Spans (ms, HIP events) of the render kernels of the most recent calls of
+ * rt_render_device on this scene, oldest first: entry i runs from the start event of the
+ * call's first pass to the end event of its last pass. Consecutive calls' launches run
+ * side by side (frames in flight), so a span also covers time the GPU spent on other
+ * calls' renders and accumulations: it is a latency, not a per-frame cost. Writes up to
+ * `max` entries, *n = entries written. Waits for those calls to finish.                 */
 int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n);
 /* Diagnostics: with RT_DEBUG_STATS=1 in the environment, renders on this scene use an
  * instrumented kernel (identical output) that tallies: [0] wave loop iterations,
@@ -211,6 +228,38 @@ int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, 
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,
                             void *stream);
+
+/* ---- persistent multi-GPU context (row tiles over ranks, gather over xGMI) ----------
+ * Rank r of n_ranks renders rows y = r, r + n, ... of every frame on device devices[r]
+ * (devices = NULL: rank r on device r) into a packed tile; tiles are gathered to rank 0's
+ * device with RCCL send/recv when every rank has its own device, and de-interleaved into
+ * the caller's frame. Scenes, streams and communicators are built once here; tiles and the
+ * gather buffer are allocated on first use of a frame size. Ranks that share a device with
+ * rank 0 ("virtual ranks", e.g. devices = {0, 0, 0, 0}: an N-way split rehearsed on one
+ * GPU) move their tiles with device copies instead of RCCL; the result is the same frame.  */
+typedef struct rt_multi rt_multi;
+enum rt_output_format { RT_OUTPUT_F32 = 0, RT_OUTPUT_RGB8 = 1 };
+int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres,
+                    const rt_material *materials, uint32_t n_materials,
+                    const int *devices, int n_ranks, rt_multi **out);
+int rt_multi_destroy(rt_multi *ctx);
+/* n_ranks, and whether the gather runs over RCCL (1) or device copies (0).              */
+int rt_multi_info(const rt_multi *ctx, int *n_ranks, int *uses_rccl);
+/* Enqueue one full frame (params' row fields and RT_FLAG_FULL_FRAME are ignored; the
+ * other flags apply on every rank) into d_out on rank 0's device: height*width*3 floats
+ * (RT_OUTPUT_F32) or bytes (RT_OUTPUT_RGB8). Rank 0 renders on `stream` (a stream of rank
+ * 0's device) and the frame is complete in `stream` order; other ranks run on their own
+ * streams. No host synchronisation, except when a frame is larger than any before it
+ * (buffers grow). Frames stream: each rank overlaps consecutive renders as
+ * rt_render_device does. One host thread per context.                                   */
+int rt_multi_render_device(rt_multi *ctx, const rt_camera *camera, const rt_params *params,
+                           uint32_t format, void *d_out, void *stream);
+/* Synchronous host-buffer frames through a context (full frame, row 0 = top); stats sum
+ * every rank's counters, kernel_ms spans the frame on rank 0's device.                   */
+int rt_multi_render_f32(rt_multi *ctx, const rt_camera *camera, const rt_params *params,
+                        float *rgb_out, rt_stats *stats);
+int rt_multi_render_rgb8(rt_multi *ctx, const rt_camera *camera, const rt_params *params,
+                         uint8_t *rgb_out, rt_stats *stats);
 
 #ifdef __cplusplus
 } /* extern "C" */

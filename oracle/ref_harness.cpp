@@ -205,7 +205,7 @@ struct args_t {
     bool corrected = false;
     std::uint32_t row0 = 0, nrows = 0, row_step = 1;
     unsigned threads = 1;
-    std::string out_f32, out_u8, dump_scene, kat, kat_out;
+    std::string out_f32, out_u8, out_ppm, dump_scene, kat, kat_out;
     std::uint32_t kat_n = 1024;
     bool timing = false;
 };
@@ -420,6 +420,7 @@ int run(int argc, char **argv)
         else if (k == "--threads") a.threads = std::max(1ul, std::stoul(nxt()));
         else if (k == "--out-f32") a.out_f32 = nxt();
         else if (k == "--out-u8") a.out_u8 = nxt();
+        else if (k == "--out-ppm") a.out_ppm = nxt();
         else if (k == "--dump-scene") a.dump_scene = nxt();
         else if (k == "--kat") a.kat = nxt();
         else if (k == "--kat-out") a.kat_out = nxt();
@@ -455,6 +456,19 @@ int run(int argc, char **argv)
     double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (!a.out_f32.empty()) { std::ofstream o(a.out_f32, std::ios::binary); o.write((const char *)f32.data(), f32.size() * 4); }
     if (!a.out_u8.empty()) { std::ofstream o(a.out_u8, std::ios::binary); o.write((const char *)u8.data(), u8.size()); }
+    if (!a.out_ppm.empty()) {
+        // the reference's own writer, app::save_to_file (src/main.cxx:87-101)
+        app::data ad;
+        ad.width = a.W;
+        ad.height = a.nrows;
+        std::vector<math::u8vec3> tex(u8.size() / 3);
+        for (size_t i = 0; i < tex.size(); ++i) {
+            tex[i].x = u8[3 * i];
+            tex[i].y = u8[3 * i + 1];
+            tex[i].z = u8[3 * i + 2];
+        }
+        app::save_to_file(a.out_ppm, ad, tex);
+    }
     if (a.timing) {
         double prim = (double)a.W * a.nrows * a.spp;
         std::printf("{\"seconds\": %.6f, \"primaries\": %.0f, \"mrays_per_s\": %.6f, \"threads\": %u, \"spheres\": %zu}\n",

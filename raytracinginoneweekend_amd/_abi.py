@@ -13,6 +13,9 @@ RT_ERR_DEVICE = -2
 RT_ERR_CAPACITY = -3
 RT_ERR_UNSUPPORTED = -4
 RT_ERR_COMM = -5
+RT_ERR_IO = -6
+
+RT_OUTPUT_F32, RT_OUTPUT_RGB8 = 0, 1
 
 RT_LAMBERT, RT_METAL, RT_DIELECTRIC = 0, 1, 2
 RT_CAMERA_REFERENCE, RT_CAMERA_CORRECTED = 0, 1

@@ -48,6 +48,20 @@ def _declare(L):
         "rt_render_multi_f32": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32,
                                           P(abi.RtCamera), P(abi.RtParams), C.c_int, P(C.c_float),
                                           P(abi.RtStats)]),
+        "rt_render_multi_rgb8": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32,
+                                           P(abi.RtCamera), P(abi.RtParams), C.c_int, P(C.c_uint8),
+                                           P(abi.RtStats)]),
+        "rt_write_ppm": (C.c_int, [C.c_char_p, P(C.c_uint8), C.c_uint32, C.c_uint32]),
+        "rt_multi_create": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32, P(C.c_int),
+                                      C.c_int, P(C.c_void_p)]),
+        "rt_multi_destroy": (C.c_int, [C.c_void_p]),
+        "rt_multi_info": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),
+        "rt_multi_render_device": (C.c_int, [C.c_void_p, P(abi.RtCamera), P(abi.RtParams), C.c_uint32, C.c_void_p,
+                                             C.c_void_p]),
+        "rt_multi_render_f32": (C.c_int, [C.c_void_p, P(abi.RtCamera), P(abi.RtParams), P(C.c_float),
+                                          P(abi.RtStats)]),
+        "rt_multi_render_rgb8": (C.c_int, [C.c_void_p, P(abi.RtCamera), P(abi.RtParams), P(C.c_uint8),
+                                           P(abi.RtStats)]),
         "rt_scene_create": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32, C.c_int,
                                       P(C.c_void_p)]),
         "rt_scene_destroy": (C.c_int, [C.c_void_p]),

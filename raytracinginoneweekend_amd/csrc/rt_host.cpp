@@ -185,6 +185,12 @@ struct rt_scene {
     static_assert(kMaxWs == 8, "ctr_dirty initialiser lists one entry per workspace");
     uint32_t next_buf = 0;  // workspace of the next render pass
     int last_ws = -1;       // workspace of the last render pass issued (its ev_done), -1 = none
+    // the caller stream of the previous call and an event after the last work enqueued on it:
+    // a call on another stream first waits for it, so the shared accumulation buffer, the
+    // compat counter and (RT_PIPELINE=0) the workspaces are never used by two streams at once
+    hipStream_t last_stream = nullptr;
+    hipEvent_t ev_tail = nullptr;
+    bool tail_valid = false;
     int cu_count = 0;
     int occ[4][2][2];  // [variant][culled][shade records in LDS] blocks per CU, -1 = unknown
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
@@ -742,6 +748,7 @@ int rt_scene_destroy(rt_scene *sc)
         if (sc->ev_done[b]) (void)hipEventDestroy(sc->ev_done[b]);
         if (sc->ev_free[b]) (void)hipEventDestroy(sc->ev_free[b]);
     }
+    if (sc->ev_tail) (void)hipEventDestroy(sc->ev_tail);
     for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr})
         if (p) (void)hipFree(p);
     for (float *p : sc->slots)
@@ -822,6 +829,8 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
                 hipEventCreateWithFlags(&sc->ev_free[b], hipEventDisableTiming) != hipSuccess)
                 rc = fail(RT_ERR_DEVICE, "rt_scene_create: stream/event creation failed");
         }
+        if (rc == RT_OK && hipEventCreateWithFlags(&sc->ev_tail, hipEventDisableTiming) != hipSuccess)
+            rc = fail(RT_ERR_DEVICE, "rt_scene_create: event creation failed");
     }
     if (rc == RT_OK) {
         hipDeviceProp_t prop;
@@ -850,17 +859,44 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     return RT_OK;
 }
 
+namespace {
+// Calls on one scene may come on different caller streams: order a call after everything the
+// previous call enqueued on its stream (the accumulation buffer and counters are
+// per scene), then remember this call's stream and its last work.
+int stream_enter(rt_scene *sc, hipStream_t st)
+{
+    if (sc->tail_valid && st != sc->last_stream) RT_HIP(hipStreamWaitEvent(st, sc->ev_tail, 0));
+    return RT_OK;
+}
+int stream_leave(rt_scene *sc, hipStream_t st)
+{
+    RT_HIP(hipEventRecord(sc->ev_tail, st));
+    sc->last_stream = st;
+    sc->tail_valid = true;
+    return RT_OK;
+}
+int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P, float *d_rgb, hipStream_t st,
+                       uint64_t *d_segments);
+} // namespace
+
 int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *params, float *d_rgb, void *stream,
                      uint64_t *d_segments)
 {
     if (!sc || !camera || !d_rgb) return fail(RT_ERR_INVALID, "rt_render_device: null argument");
     if (int rc = check_params(params); rc != RT_OK) return rc;
-    const rt_params P = *params;
     hipStream_t st = static_cast<hipStream_t>(stream);
     RT_HIP(hipSetDevice(sc->device));
+    if (int rc = stream_enter(sc, st); rc != RT_OK) return rc;
+    const int rc = (params->flags & RT_FLAG_CUDA_COMPAT) ? render_compat(sc, camera, *params, d_rgb, st, d_segments)
+                                                         : render_device_impl(sc, camera, *params, d_rgb, st, d_segments);
+    if (rc != RT_OK) return rc;
+    return stream_leave(sc, st);
+}
 
-    if (P.flags & RT_FLAG_CUDA_COMPAT) return render_compat(sc, camera, P, d_rgb, st, d_segments);
-
+namespace {
+int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P, float *d_rgb, hipStream_t st,
+                       uint64_t *d_segments)
+{
     rt::KParams k{};
     for (int c = 0; c < 3; ++c) {
         k.org[c] = camera->origin[c];
@@ -1052,7 +1088,6 @@ int rt_render_device(rt_scene *sc, const rt_camera *camera, const rt_params *par
     return RT_OK;
 }
 
-namespace {
 int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, float *d_rgb, hipStream_t st,
                   uint64_t *d_segments)
 {
@@ -1279,139 +1314,389 @@ const rccl_api &rccl()
 }
 } // namespace
 
+// Persistent multi-GPU context (rt_multi_*): rank r of N renders the rows y = r, r + N, ...
+// (interleaved single rows balance sky against ground) on its device into a packed tile;
+// optionally the gamma/u8 epilogue runs on the tile (3 B per pixel instead of 12 over xGMI);
+// the tiles are gathered to rank 0's device and de-interleaved into the caller's frame.
+// Everything that does not depend on the frame is built once at rt_multi_create: per-device
+// scenes, rank streams, the RCCL communicators (ncclCommInitAll over the distinct devices), the
+// segment counters; tiles and the gather buffer grow on first use of a frame size. Ranks that
+// share a device with rank 0 ("virtual ranks": a one-GPU rehearsal of an N-way split) move
+// their tile with a device copy where RCCL would send/recv; the tile layout, the gather buffer
+// and the de-interleave are the same code either way.
+struct rt_multi {
+    int n = 0;
+    std::vector<int> dev;
+    bool rccl = false;  // every rank on its own device: gather over RCCL
+    std::vector<rt_scene *> sc;
+    std::vector<hipStream_t> st;        // rank r > 0: its stream (rank 0 runs on the caller's stream)
+    std::vector<ncclComm_t> comm;
+    std::vector<void *> tile;           // f32 tile per rank, on its device
+    std::vector<size_t> tile_bytes;
+    std::vector<void *> tile8;          // u8 tile per rank (RT_OUTPUT_RGB8)
+    std::vector<size_t> tile8_bytes;
+    std::vector<uint64_t *> seg;        // per rank: {segments, sphere tests, box tests}
+    void *gather = nullptr;             // on rank 0's device: N slots of the largest tile
+    size_t gather_bytes = 0;
+    std::vector<hipEvent_t> ev_ready;   // virtual rank r: its tile is complete
+    hipEvent_t ev_copied = nullptr;     // caller stream: virtual ranks' tiles copied out
+    bool copied_valid = false;
+    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
+};
+
+namespace {
+
+int multi_fail_destroy(rt_multi *m, int rc);
+
+// ensure() without the device-wide synchronisation: the buffers of a context grow only
+// between frames the caller has already synchronised (rt_multi_render_* documents it)
+int grow(int device, void **ptr, size_t *have, size_t want)
+{
+    if (*have >= want && *ptr) return RT_OK;
+    RT_HIP(hipSetDevice(device));
+    if (*ptr) {
+        RT_HIP(hipDeviceSynchronize());
+        RT_HIP(hipFree(*ptr));
+        *ptr = nullptr;
+        *have = 0;
+    }
+    RT_HIP(hipMalloc(ptr, std::max<size_t>(want, 256)));
+    *have = want;
+    return RT_OK;
+}
+
+uint32_t multi_rows(uint32_t H, int n, int r)
+{
+    return static_cast<uint32_t>(r) < H ? (H - static_cast<uint32_t>(r) + static_cast<uint32_t>(n) - 1) / static_cast<uint32_t>(n) : 0u;
+}
+
+} // namespace
+
 extern "C" {
 
-int rt_render_multi_f32(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
-                        uint32_t n_materials, const rt_camera *camera, const rt_params *params, int ngpu,
-                        float *rgb_out, rt_stats *stats)
+int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
+                    const int *devices, int n_ranks, rt_multi **out)
 {
-    if (!camera || !rgb_out) return fail(RT_ERR_INVALID, "rt_render_multi_f32: null argument");
-    if (int rc = check_params(params); rc != RT_OK) return rc;
-    const auto t0 = std::chrono::steady_clock::now();
+    if (!out) return fail(RT_ERR_INVALID, "rt_multi_create: null output");
+    *out = nullptr;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_DEVICE, "rt_render_multi_f32: no HIP device");
-    const int N = ngpu <= 0 ? ndev : std::min(ngpu, ndev);
-    const rt_params base = *params;
-    const uint32_t W = base.width, H = base.height;
-    // rank r renders rows y = r, r + N, ... (rows of the whole image; row_offset/num_rows ignored)
-    std::vector<uint32_t> rows(N);
-    for (int r = 0; r < N; ++r) rows[r] = static_cast<uint32_t>(r) < H ? (H - r + N - 1) / N : 0;
-    std::vector<rt_scene *> sc(N, nullptr);
-    std::vector<hipStream_t> st(N, nullptr);
-    std::vector<float *> tile(N, nullptr), recv(N, nullptr);
-    std::vector<uint64_t *> seg(N, nullptr);
-    std::vector<hipEvent_t> e0(N, nullptr), e1(N, nullptr);
-    std::vector<ncclComm_t> comms;
-    float *frame = nullptr;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_DEVICE, "rt_multi_create: no HIP device");
+    const int N = n_ranks <= 0 ? ndev : n_ranks;
+    if (!devices && N > ndev) return fail(RT_ERR_INVALID, "rt_multi_create: more ranks than devices (pass a device list)");
+    if (N > 64) return fail(RT_ERR_INVALID, "rt_multi_create: at most 64 ranks");
+    rt_multi *m = new rt_multi();
+    m->n = N;
+    for (int r = 0; r < N; ++r) {
+        const int d = devices ? devices[r] : r;
+        if (d < 0 || d >= ndev) {
+            delete m;
+            return fail(RT_ERR_INVALID, "rt_multi_create: bad device index");
+        }
+        m->dev.push_back(d);
+    }
+    m->rccl = N > 1;
+    for (int r = 0; r < N && m->rccl; ++r)
+        for (int q = 0; q < r; ++q)
+            if (m->dev[q] == m->dev[r]) m->rccl = false;
+    m->sc.assign(N, nullptr);
+    m->st.assign(N, nullptr);
+    m->tile.assign(N, nullptr);
+    m->tile_bytes.assign(N, 0);
+    m->tile8.assign(N, nullptr);
+    m->tile8_bytes.assign(N, 0);
+    m->seg.assign(N, nullptr);
+    m->ev_ready.assign(N, nullptr);
     int rc = RT_OK;
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
         return rc == RT_OK;
     };
     for (int r = 0; r < N && rc == RT_OK; ++r) {
-        rc = rt_scene_create(spheres, n_spheres, materials, n_materials, r, &sc[r]);
+        rc = rt_scene_create(spheres, n_spheres, materials, n_materials, m->dev[r], &m->sc[r]);
         if (rc != RT_OK) break;
-        chk(hipSetDevice(r), "hipSetDevice");
-        chk(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking), "hipStreamCreate");
-        chk(hipMalloc(&tile[r], std::max<size_t>(1, static_cast<size_t>(rows[r]) * W * 3) * 4), "hipMalloc");
-        chk(hipMalloc(&seg[r], 24), "hipMalloc");
-        chk(hipMemsetAsync(seg[r], 0, 24, st[r]), "hipMemsetAsync");
-        chk(hipEventCreate(&e0[r]), "hipEventCreate");
-        chk(hipEventCreate(&e1[r]), "hipEventCreate");
-        if (r == 0) chk(hipMalloc(&frame, static_cast<size_t>(H) * W * 3 * 4), "hipMalloc");
-        if (r > 0 && rc == RT_OK) {
-            chk(hipSetDevice(0), "hipSetDevice");
-            chk(hipMalloc(&recv[r], std::max<size_t>(1, static_cast<size_t>(rows[r]) * W * 3) * 4), "hipMalloc");
+        chk(hipSetDevice(m->dev[r]), "hipSetDevice");
+        if (r > 0) chk(hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking), "hipStreamCreate");
+        chk(hipMalloc((void **)&m->seg[r], 3 * sizeof(uint64_t)), "hipMalloc");
+        chk(hipMemset(m->seg[r], 0, 3 * sizeof(uint64_t)), "hipMemset");
+        chk(hipEventCreateWithFlags(&m->ev_ready[r], hipEventDisableTiming), "hipEventCreate");
+    }
+    if (rc == RT_OK) {
+        chk(hipSetDevice(m->dev[0]), "hipSetDevice");
+        chk(hipEventCreateWithFlags(&m->ev_copied, hipEventDisableTiming), "hipEventCreate");
+        chk(hipEventCreate(&m->ev_t0), "hipEventCreate");
+        chk(hipEventCreate(&m->ev_t1), "hipEventCreate");
+    }
+    if (rc == RT_OK && m->rccl) {
+        const rccl_api &api = rccl();
+        if (!api.ok) {
+            rc = fail(RT_ERR_COMM, "rt_multi_create: librccl.so.1 not loadable");
+        } else {
+            m->comm.assign(N, nullptr);
+            const ncclResult_t nr = api.comm_init_all(m->comm.data(), N, m->dev.data());
+            if (nr != ncclSuccess) {
+                m->comm.clear();
+                rc = fail(RT_ERR_COMM, std::string("ncclCommInitAll: ") + api.error_string(nr));
+            }
         }
     }
-    // render every tile concurrently
-    for (int r = 0; r < N && rc == RT_OK; ++r) {
-        if (!rows[r]) continue;
+    if (rc != RT_OK) return multi_fail_destroy(m, rc);
+    (void)hipSetDevice(m->dev[0]);
+    *out = m;
+    return RT_OK;
+}
+
+int rt_multi_destroy(rt_multi *m)
+{
+    if (!m) return RT_OK;
+    for (int r = 0; r < m->n; ++r) {
+        (void)hipSetDevice(m->dev[r]);
+        if (m->st[r]) (void)hipStreamSynchronize(m->st[r]);
+    }
+    (void)hipSetDevice(m->dev[0]);
+    (void)hipDeviceSynchronize();
+    for (auto c : m->comm)
+        if (c) rccl().comm_destroy(c);
+    for (int r = 0; r < m->n; ++r) {
+        (void)hipSetDevice(m->dev[r]);
+        if (m->tile[r]) (void)hipFree(m->tile[r]);
+        if (m->tile8[r]) (void)hipFree(m->tile8[r]);
+        if (m->seg[r]) (void)hipFree(m->seg[r]);
+        if (m->ev_ready[r]) (void)hipEventDestroy(m->ev_ready[r]);
+        if (m->st[r]) (void)hipStreamDestroy(m->st[r]);
+        if (m->sc[r]) rt_scene_destroy(m->sc[r]);
+    }
+    (void)hipSetDevice(m->dev[0]);
+    if (m->gather) (void)hipFree(m->gather);
+    for (hipEvent_t e : {m->ev_copied, m->ev_t0, m->ev_t1})
+        if (e) (void)hipEventDestroy(e);
+    delete m;
+    return RT_OK;
+}
+
+int rt_multi_info(const rt_multi *m, int *n_ranks, int *uses_rccl)
+{
+    if (!m) return fail(RT_ERR_INVALID, "rt_multi_info: null context");
+    if (n_ranks) *n_ranks = m->n;
+    if (uses_rccl) *uses_rccl = m->rccl ? 1 : 0;
+    return RT_OK;
+}
+
+int rt_multi_render_device(rt_multi *m, const rt_camera *camera, const rt_params *params, uint32_t format,
+                           void *d_out, void *stream)
+{
+    if (!m || !camera || !d_out) return fail(RT_ERR_INVALID, "rt_multi_render_device: null argument");
+    if (format != RT_OUTPUT_F32 && format != RT_OUTPUT_RGB8) return fail(RT_ERR_INVALID, "rt_multi_render_device: bad format");
+    if (int rc = check_params(params); rc != RT_OK) return rc;
+    const rt_params base = *params;
+    const int N = m->n;
+    const uint32_t W = base.width, H = base.height;
+    const size_t es = format == RT_OUTPUT_F32 ? 4u : 1u;
+    const size_t row_vals = static_cast<size_t>(W) * 3u;
+    const uint32_t rows_max = multi_rows(H, N, 0);
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    // buffers (grow only: a new, larger frame size costs one synchronisation)
+    for (int r = 0; r < N; ++r) {
+        const size_t rows = multi_rows(H, N, r);
+        if (int rc = grow(m->dev[r], &m->tile[r], &m->tile_bytes[r], std::max<size_t>(rows, 1) * row_vals * 4u); rc) return rc;
+        if (format == RT_OUTPUT_RGB8)
+            if (int rc = grow(m->dev[r], &m->tile8[r], &m->tile8_bytes[r], std::max<size_t>(rows, 1) * row_vals); rc) return rc;
+    }
+    if (N > 1)
+        if (int rc = grow(m->dev[0], &m->gather, &m->gather_bytes, static_cast<size_t>(N) * rows_max * row_vals * es); rc)
+            return rc;
+    auto tile_of = [&](int r) -> void * { return format == RT_OUTPUT_F32 ? m->tile[r] : m->tile8[r]; };
+    // 1. every rank renders its rows (rank 0 on the caller's stream); virtual ranks wait until
+    //    the caller stream has copied their previous tile out
+    for (int r = 0; r < N; ++r) {
+        const uint32_t rows = multi_rows(H, N, r);
+        if (!rows) continue;
         rt_params p = base;
         p.row_offset = static_cast<uint32_t>(r);
         p.row_stride = static_cast<uint32_t>(N);
-        p.num_rows = rows[r];
-        p.flags &= ~RT_FLAG_FULL_FRAME;
-        chk(hipSetDevice(r), "hipSetDevice");
-        chk(hipEventRecord(e0[r], st[r]), "hipEventRecord");
-        if (rc == RT_OK) rc = rt_render_device(sc[r], camera, &p, tile[r], st[r], seg[r]);
-        chk(hipEventRecord(e1[r], st[r]), "hipEventRecord");
+        p.num_rows = rows;
+        p.flags &= ~static_cast<uint32_t>(RT_FLAG_FULL_FRAME);
+        hipStream_t rs = r == 0 ? cs : m->st[r];
+        RT_HIP(hipSetDevice(m->dev[r]));
+        if (r > 0 && !m->rccl && m->copied_valid) RT_HIP(hipStreamWaitEvent(rs, m->ev_copied, 0));
+        if (int rc = rt_render_device(m->sc[r], camera, &p, static_cast<float *>(m->tile[r]), rs, m->seg[r]); rc) return rc;
+        if (format == RT_OUTPUT_RGB8)
+            RT_HIP(rt::launch_epilogue(static_cast<const float *>(m->tile[r]), static_cast<uint8_t *>(m->tile8[r]),
+                                       static_cast<uint64_t>(rows) * row_vals, rs));
+        if (r > 0 && !m->rccl) RT_HIP(hipEventRecord(m->ev_ready[r], rs));
     }
-    // gather the tiles to device 0 over RCCL (one point-to-point transfer per peer link)
-    if (rc == RT_OK && N > 1) {
+    // 2. the gather: tile r -> slot r of the gather buffer on rank 0's device
+    const size_t slot_bytes = static_cast<size_t>(rows_max) * row_vals * es;
+    if (N > 1 && m->rccl) {
         const rccl_api &api = rccl();
-        if (!api.ok) rc = fail(RT_ERR_COMM, "rt_render_multi_f32: librccl.so.1 not loadable");
-        std::vector<int> devs(N);
-        for (int r = 0; r < N; ++r) devs[r] = r;
-        comms.assign(N, nullptr);
-        if (rc == RT_OK) {
-            ncclResult_t nr = api.comm_init_all(comms.data(), N, devs.data());
-            if (nr != ncclSuccess) rc = fail(RT_ERR_COMM, std::string("ncclCommInitAll: ") + api.error_string(nr));
+        ncclResult_t nr = api.group_start();
+        for (int r = 1; r < N && nr == ncclSuccess; ++r) {
+            const size_t cnt = static_cast<size_t>(multi_rows(H, N, r)) * row_vals;
+            if (!cnt) continue;
+            const ncclDataType_t ty = format == RT_OUTPUT_F32 ? ncclFloat : ncclUint8;
+            nr = api.send(tile_of(r), cnt, ty, 0, m->comm[r], m->st[r]);
+            if (nr == ncclSuccess)
+                nr = api.recv(static_cast<char *>(m->gather) + r * slot_bytes, cnt, ty, r, m->comm[0], cs);
         }
-        if (rc == RT_OK) {
-            ncclResult_t nr = api.group_start();
-            for (int r = 1; r < N && nr == ncclSuccess; ++r) {
-                if (!rows[r]) continue;
-                const size_t cnt = static_cast<size_t>(rows[r]) * W * 3;
-                nr = api.send(tile[r], cnt, ncclFloat, 0, comms[r], st[r]);
-                if (nr == ncclSuccess) nr = api.recv(recv[r], cnt, ncclFloat, r, comms[0], st[0]);
-            }
-            ncclResult_t ne = api.group_end();
-            if (nr == ncclSuccess) nr = ne;
-            if (nr != ncclSuccess) rc = fail(RT_ERR_COMM, std::string("RCCL gather: ") + api.error_string(nr));
+        const ncclResult_t ne = api.group_end();
+        if (nr == ncclSuccess) nr = ne;
+        if (nr != ncclSuccess) return fail(RT_ERR_COMM, std::string("RCCL gather: ") + api.error_string(nr));
+    } else if (N > 1) {
+        RT_HIP(hipSetDevice(m->dev[0]));
+        for (int r = 1; r < N; ++r) {
+            const size_t bytes = static_cast<size_t>(multi_rows(H, N, r)) * row_vals * es;
+            if (!bytes) continue;
+            RT_HIP(hipStreamWaitEvent(cs, m->ev_ready[r], 0));
+            RT_HIP(hipMemcpyAsync(static_cast<char *>(m->gather) + r * slot_bytes, tile_of(r), bytes,
+                                  hipMemcpyDeviceToDevice, cs));
         }
+        RT_HIP(hipEventRecord(m->ev_copied, cs));
+        m->copied_valid = true;
     }
-    // de-interleave on device 0: frame row r + i*N <- tile r row i (one strided copy per rank)
-    if (rc == RT_OK) {
-        chk(hipSetDevice(0), "hipSetDevice");
-        const size_t row_bytes = static_cast<size_t>(W) * 3 * 4;
-        for (int r = 0; r < N && rc == RT_OK; ++r) {
-            if (!rows[r]) continue;
-            chk(hipMemcpy2DAsync(frame + static_cast<size_t>(r) * W * 3, row_bytes * N, r == 0 ? tile[0] : recv[r],
-                                 row_bytes, row_bytes, rows[r], hipMemcpyDeviceToDevice, st[0]),
-                "hipMemcpy2DAsync");
-        }
-        chk(hipMemcpyAsync(rgb_out, frame, static_cast<size_t>(H) * W * 3 * 4, hipMemcpyDeviceToHost, st[0]),
-            "hipMemcpyAsync");
+    // 3. de-interleave on rank 0's device: frame row r + i N <- tile r row i
+    RT_HIP(hipSetDevice(m->dev[0]));
+    const size_t row_bytes = row_vals * es;
+    for (int r = 0; r < N; ++r) {
+        const uint32_t rows = multi_rows(H, N, r);
+        if (!rows) continue;
+        const void *src = r == 0 ? tile_of(0) : static_cast<const void *>(static_cast<char *>(m->gather) + r * slot_bytes);
+        RT_HIP(hipMemcpy2DAsync(static_cast<char *>(d_out) + r * row_bytes, row_bytes * N, src, row_bytes, row_bytes,
+                                rows, hipMemcpyDeviceToDevice, cs));
     }
+    return RT_OK;
+}
+
+} // extern "C"
+
+namespace {
+
+int multi_fail_destroy(rt_multi *m, int rc)
+{
+    const std::string msg = g_error;
+    rt_multi_destroy(m);
+    g_error = msg;
+    return rc;
+}
+
+// Synchronous host-buffer frame through a context: every rank's counters are zeroed, the frame
+// is enqueued on an internal stream of rank 0's device, copied to `out` and timed.
+int multi_render_host(rt_multi *m, const rt_camera *camera, const rt_params *params, uint32_t format, void *out,
+                      rt_stats *stats)
+{
+    if (!m || !camera || !out) return fail(RT_ERR_INVALID, "rt_multi_render: null argument");
+    if (int rc = check_params(params); rc != RT_OK) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t es = format == RT_OUTPUT_F32 ? 4u : 1u;
+    const size_t bytes = static_cast<size_t>(params->width) * params->height * 3u * es;
+    for (int r = 0; r < m->n; ++r) {
+        RT_HIP(hipSetDevice(m->dev[r]));
+        RT_HIP(hipMemset(m->seg[r], 0, 3 * sizeof(uint64_t)));
+    }
+    RT_HIP(hipSetDevice(m->dev[0]));
+    void *d_out = nullptr;
+    hipStream_t cs = nullptr;
+    RT_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    int rc = RT_OK;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+        return rc == RT_OK;
+    };
+    chk(hipMalloc(&d_out, bytes), "hipMalloc");
+    if (rc == RT_OK) chk(hipEventRecord(m->ev_t0, cs), "hipEventRecord");
+    if (rc == RT_OK) rc = rt_multi_render_device(m, camera, params, format, d_out, cs);
+    (void)hipSetDevice(m->dev[0]);
+    if (rc == RT_OK) chk(hipEventRecord(m->ev_t1, cs), "hipEventRecord");
+    if (rc == RT_OK) chk(hipMemcpyAsync(out, d_out, bytes, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
+    for (int r = 0; r < m->n; ++r) {
+        (void)hipSetDevice(m->dev[r]);
+        if (m->st[r]) chk(hipStreamSynchronize(m->st[r]), "hipStreamSynchronize");
+    }
+    (void)hipSetDevice(m->dev[0]);
+    chk(hipStreamSynchronize(cs), "hipStreamSynchronize");
     uint64_t segs[3] = {0, 0, 0};
-    double kms = 0.0;
-    for (int r = 0; r < N; ++r) {
-        if (rc == RT_OK && st[r]) {
-            chk(hipSetDevice(r), "hipSetDevice");
-            chk(hipStreamSynchronize(st[r]), "hipStreamSynchronize");
-            uint64_t v[3] = {0, 0, 0};
-            chk(hipMemcpy(v, seg[r], 24, hipMemcpyDeviceToHost), "hipMemcpy");
-            float ms = 0.f;
-            if (rows[r]) chk(hipEventElapsedTime(&ms, e0[r], e1[r]), "hipEventElapsedTime");
-            for (int i = 0; i < 3; ++i) segs[i] += v[i];
-            kms = std::max(kms, static_cast<double>(ms));
-        }
+    for (int r = 0; r < m->n && rc == RT_OK; ++r) {
+        uint64_t v[3];
+        (void)hipSetDevice(m->dev[r]);
+        chk(hipMemcpy(v, m->seg[r], sizeof v, hipMemcpyDeviceToHost), "hipMemcpy");
+        for (int i = 0; i < 3; ++i) segs[i] += v[i];
     }
-    for (auto c : comms)
-        if (c) rccl().comm_destroy(c);
-    for (int r = 0; r < N; ++r) {
-        (void)hipSetDevice(r);
-        if (e0[r]) (void)hipEventDestroy(e0[r]);
-        if (e1[r]) (void)hipEventDestroy(e1[r]);
-        if (tile[r]) (void)hipFree(tile[r]);
-        if (seg[r]) (void)hipFree(seg[r]);
-        if (st[r]) (void)hipStreamDestroy(st[r]);
-        if (sc[r]) rt_scene_destroy(sc[r]);
-    }
-    (void)hipSetDevice(0);
-    for (int r = 1; r < N; ++r)
-        if (recv[r]) (void)hipFree(recv[r]);
-    if (frame) (void)hipFree(frame);
+    (void)hipSetDevice(m->dev[0]);
+    float ms = 0.f;
+    if (rc == RT_OK) chk(hipEventElapsedTime(&ms, m->ev_t0, m->ev_t1), "hipEventElapsedTime");
+    if (d_out) (void)hipFree(d_out);
+    (void)hipStreamDestroy(cs);
     if (rc == RT_OK && stats) {
-        stats->primaries = static_cast<uint64_t>(W) * H * base.spp;
+        stats->primaries = static_cast<uint64_t>(params->width) * params->height * params->spp;
         stats->segments = segs[0];
         stats->sphere_tests = segs[1];
         stats->box_tests = segs[2];
-        stats->kernel_ms = kms;
+        stats->kernel_ms = ms;
         stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return rc;
+}
+
+int render_multi_once(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
+                      const rt_camera *camera, const rt_params *params, int ngpu, uint32_t format, void *out,
+                      rt_stats *stats)
+{
+    if (!camera || !out) return fail(RT_ERR_INVALID, "rt_render_multi: null argument");
+    if (int rc = check_params(params); rc != RT_OK) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_DEVICE, "rt_render_multi: no HIP device");
+    rt_multi *m = nullptr;
+    if (int rc = rt_multi_create(spheres, n_spheres, materials, n_materials, nullptr,
+                                 ngpu <= 0 ? ndev : std::min(ngpu, ndev), &m); rc)
+        return rc;
+    const int rc = multi_render_host(m, camera, params, format, out, stats);
+    const std::string msg = g_error;
+    rt_multi_destroy(m);
+    g_error = msg;
+    return rc;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_multi_render_f32(rt_multi *m, const rt_camera *camera, const rt_params *params, float *rgb_out, rt_stats *stats)
+{
+    return multi_render_host(m, camera, params, RT_OUTPUT_F32, rgb_out, stats);
+}
+
+int rt_multi_render_rgb8(rt_multi *m, const rt_camera *camera, const rt_params *params, uint8_t *rgb_out,
+                         rt_stats *stats)
+{
+    return multi_render_host(m, camera, params, RT_OUTPUT_RGB8, rgb_out, stats);
+}
+
+int rt_render_multi_f32(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
+                        uint32_t n_materials, const rt_camera *camera, const rt_params *params, int ngpu,
+                        float *rgb_out, rt_stats *stats)
+{
+    return render_multi_once(spheres, n_spheres, materials, n_materials, camera, params, ngpu, RT_OUTPUT_F32, rgb_out,
+                             stats);
+}
+
+int rt_render_multi_rgb8(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
+                         uint32_t n_materials, const rt_camera *camera, const rt_params *params, int ngpu,
+                         uint8_t *rgb_out, rt_stats *stats)
+{
+    return render_multi_once(spheres, n_spheres, materials, n_materials, camera, params, ngpu, RT_OUTPUT_RGB8, rgb_out,
+                             stats);
+}
+
+// app::save_to_file, src/main.cxx:87-101: "P6\n<width> <height>\n255\n", then the texels.
+int rt_write_ppm(const char *path, const uint8_t *rgb, uint32_t width, uint32_t height)
+{
+    if (!path || (!rgb && width && height)) return fail(RT_ERR_INVALID, "rt_write_ppm: null argument");
+    std::FILE *f = std::fopen(path, "wb");
+    if (!f) return fail(RT_ERR_IO, std::string("rt_write_ppm: bad file ") + path);
+    const std::string hdr = "P6\n" + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
+    const size_t n = static_cast<size_t>(width) * height * 3u;
+    const bool ok = std::fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size() && (n == 0 || std::fwrite(rgb, 1, n, f) == n);
+    const bool closed = std::fclose(f) == 0;
+    if (!ok || !closed) return fail(RT_ERR_IO, std::string("rt_write_ppm: write failed: ") + path);
+    return RT_OK;
 }
 
 } // extern "C"

@@ -3,9 +3,11 @@
 render_f32 / render_rgb8   synchronous, host numpy buffers (rt_render_f32 / rt_render_rgb8)
 DeviceScene.render         async on a caller stream into a device buffer (rt_render_device),
                            the path bench.py times with inputs resident in HBM
-save_ppm                   app::save_to_file (src/main.cxx:87-101)
+MultiContext               row tiles over ranks (devices), gathered to rank 0 (rt_multi_*)
+save_ppm                   app::save_to_file (src/main.cxx:87-101), rt_write_ppm
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -71,6 +73,68 @@ def render_multi_f32(scene, params, ngpu=0, camera=None):
                                     abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), C.byref(_cam(camera, params)),
                                     C.byref(params), ngpu, abi.ptr(out, C.POINTER(C.c_float)), C.byref(st)))
     return out, st
+
+
+def render_multi_rgb8(scene, params, ngpu=0, camera=None):
+    """As render_multi_f32 with the gamma/u8 epilogue on every rank before the gather."""
+    s, m = _scene_arrays(scene)
+    out = np.zeros((params.height, params.width, 3), dtype=np.uint8)
+    st = abi.RtStats()
+    check(lib().rt_render_multi_rgb8(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
+                                     abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), C.byref(_cam(camera, params)),
+                                     C.byref(params), ngpu, abi.ptr(out, C.POINTER(C.c_uint8)), C.byref(st)))
+    return out, st
+
+
+class MultiContext:
+    """Persistent row-tile context over ranks (rt_multi_create): rank r renders rows r, r+N, ...
+    on devices[r]; tiles are gathered to rank 0 (RCCL when every rank has its own device,
+    device copies for ranks sharing rank 0's device) and de-interleaved into the frame."""
+
+    def __init__(self, scene, devices=None, n_ranks=0):
+        s, m = _scene_arrays(scene)
+        h = C.c_void_p()
+        devs = None
+        if devices is not None:
+            devs = (C.c_int * len(devices))(*devices)
+            n_ranks = len(devices)
+        check(lib().rt_multi_create(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
+                                    abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), devs, n_ranks, C.byref(h)))
+        self.handle = h
+        n, r = C.c_int(0), C.c_int(0)
+        check(lib().rt_multi_info(h, C.byref(n), C.byref(r)))
+        self.n_ranks, self.uses_rccl = n.value, bool(r.value)
+
+    def render_f32(self, params, camera=None):
+        out = np.zeros((params.height, params.width, 3), dtype=np.float32)
+        st = abi.RtStats()
+        check(lib().rt_multi_render_f32(self.handle, C.byref(_cam(camera, params)), C.byref(params),
+                                        abi.ptr(out, C.POINTER(C.c_float)), C.byref(st)))
+        return out, st
+
+    def render_rgb8(self, params, camera=None):
+        out = np.zeros((params.height, params.width, 3), dtype=np.uint8)
+        st = abi.RtStats()
+        check(lib().rt_multi_render_rgb8(self.handle, C.byref(_cam(camera, params)), C.byref(params),
+                                         abi.ptr(out, C.POINTER(C.c_uint8)), C.byref(st)))
+        return out, st
+
+    def render_device(self, camera, params, d_out, stream=None, rgb8=False):
+        """Enqueue a full frame into device pointer d_out on rank 0's device, `stream` order."""
+        check(lib().rt_multi_render_device(self.handle, C.byref(_cam(camera, params)), C.byref(params),
+                                           abi.RT_OUTPUT_RGB8 if rgb8 else abi.RT_OUTPUT_F32, C.c_void_p(d_out),
+                                           C.c_void_p(stream or 0)))
+
+    def close(self):
+        if self.handle:
+            lib().rt_multi_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def render_cuda_impl(width, height):
@@ -144,9 +208,8 @@ def epilogue_rgb8_device(d_rgb, d_out, n_pixels, stream=None):
 
 
 def save_ppm(path, rgb8):
-    """app::save_to_file: binary P6, 'P6\\n<w> <h>\\n255\\n' then texels (src/main.cxx:87-101)."""
+    """app::save_to_file (src/main.cxx:87-101) through rt_write_ppm: binary P6,
+    'P6\\n<w> <h>\\n255\\n' then the (h, w, 3) texels."""
     rgb8 = np.ascontiguousarray(rgb8, dtype=np.uint8)
     h, w, _ = rgb8.shape
-    with open(path, "wb") as f:
-        f.write(f"P6\n{w} {h}\n255\n".encode())
-        f.write(rgb8.tobytes())
+    check(lib().rt_write_ppm(os.fsencode(path), abi.ptr(rgb8, C.POINTER(C.c_uint8)), w, h))

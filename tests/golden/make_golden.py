@@ -36,7 +36,15 @@ RENDERS = [
                                       "--row0", "100", "--row-step", "360", "--rows", "2"], "pcg"),
     ("huge_1280x720_row300_s2_corr", ["--scene", "@huge", "--w", "1280", "--h", "720", "--spp", "2",
                                       "--row0", "300", "--rows", "1", "--camera", "corrected"], "pcg"),
+    # one full-spp row of config 4 (3840x2160 @256spp; 13 render passes on one GPU) and of
+    # config 5 (1280x720 @1024spp; 6 passes): the multi-pass frames checked against the reference
+    ("c4_huge_3840x2160_row1133_s256", ["--scene", "@huge", "--w", "3840", "--h", "2160", "--spp", "256",
+                                        "--row0", "1133", "--rows", "1"], "pcg"),
+    ("c5_huge_1280x720_row377_s1024", ["--scene", "@huge", "--w", "1280", "--h", "720", "--spp", "1024",
+                                       "--row0", "377", "--rows", "1"], "pcg"),
 ]
+# renders whose u8 frame is also written by the reference's own PPM writer (app::save_to_file)
+PPM = {"c1_simple_200x100_s1"}
 KATS = [("kat_hit", "hit", "@huge", 2048), ("kat_scatter", "scatter", "@huge", 2048),
         ("kat_camera", "camera", "simple", 512), ("kat_misc", "misc", "simple", 1024)]
 
@@ -66,8 +74,9 @@ def main():
         f32 = os.path.join(HERE, name + ".f32")
         u8 = os.path.join(HERE, name + ".u8")
         exe = pcg if kind == "pcg" else mt
+        ppm = os.path.join(HERE, name + ".ppm") if name in PPM else None
         subprocess.run([exe] + args + ["--seed", "1234", "--threads", "8", "--out-f32", f32,
-                                       "--out-u8", u8], check=True)
+                                       "--out-u8", u8] + (["--out-ppm", ppm] if ppm else []), check=True)
         a = dict(zip(args[::2], args[1::2]))
         scene = "huge" if a["--scene"] == huge else "simple"
         W, H = int(a["--w"]), int(a["--h"])
@@ -78,6 +87,8 @@ def main():
             "depth": int(a.get("--depth", 64)), "camera": a.get("--camera", "reference"),
             "row_offset": row0, "row_stride": step, "num_rows": rows, "rng": kind, "seed": 1234,
             "f32": name + ".f32", "u8": name + ".u8", "sha256_f32": sha(f32), "sha256_u8": sha(u8)}
+        if ppm:
+            manifest["renders"][name].update({"ppm": name + ".ppm", "sha256_ppm": sha(ppm)})
     for name, kat, scene, n in KATS:
         out = os.path.join(HERE, name + ".bin")
         sc = huge if scene == "@huge" else scene

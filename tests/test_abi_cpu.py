@@ -125,6 +125,21 @@ def test_save_ppm(tmp_path):
     assert raw.startswith(b"P6\n3 2\n255\n") and raw[len(b"P6\n3 2\n255\n"):] == img.tobytes()
 
 
+def test_write_ppm_reproduces_reference_file(tmp_path):
+    """rt_write_ppm on the reference's u8 frame of config 1 is byte for byte the file the
+    reference's app::save_to_file wrote (tests/golden/c1_simple_200x100_s1.ppm)."""
+    meta, _, u8 = G.render("c1_simple_200x100_s1")
+    p = tmp_path / "image.ppm"
+    rt.save_ppm(str(p), u8.reshape(meta["num_rows"], meta["width"], 3))
+    assert p.read_bytes() == open(os.path.join(G.GOLDEN, meta["ppm"]), "rb").read()
+
+
+def test_write_ppm_bad_path_fails_loudly(tmp_path):
+    with pytest.raises(rt.RtError) as e:
+        rt.save_ppm(str(tmp_path / "no" / "such" / "dir.ppm"), np.zeros((1, 1, 3), np.uint8))
+    assert e.value.status == abi.RT_ERR_IO
+
+
 # ---- the reference's CUDA variant (RT_FLAG_CUDA_COMPAT; src/CUDA/cuda_impl.cu) -------------
 def test_cuda_variant_scene_and_camera():
     """rt_scene_cuda / rt_camera_cuda: cuda_impl.cu:425-437 and :371-375, the camera basis bit

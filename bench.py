@@ -16,7 +16,12 @@ finish (render + accumulate + gather), timed synchronously after the timed loop.
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 The cpu_baseline leg (rank 0, N=1) times the REFERENCE's own CPU path (oracle/_ref, built
-from /root/reference) on a bounded row subset of the same workload, on this host's cores.
+from /root/reference) on a bounded row subset of the same workload, on this host's cores, with
+a single-thread figure and the optimized CPU restatement beside it.
+
+roofline: executed sphere + box test FLOP per frame over the frame period (ms_per_step) against
+the f32 vector peak; traffic and VALU issue come from a rocprofv3 --pmc summary of the SAME
+build (profiles/pmc_render_c3.json, stamped with the library's sha256; dropped otherwise).
 """
 import argparse
 import json
@@ -66,13 +71,20 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=240, help="rows in the CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this job may use (cpu_info)")
     ap.add_argument("--rehearse-world", type=int, default=0,
                     help="diagnostic, 1 GPU: render only rank 0's rows of an N-way split (no gather) to "
                          "estimate one rank's frame time at N GPUs; not a bench line")
-    ap.add_argument("--hw-queues", type=int, default=8,
-                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = leave the environment): "
-                         "the library runs one render stream fewer than this, 2..4 (rt_host.cpp pipeline_env)")
+    ap.add_argument("--hw-queues", type=int, default=-1,
+                    help="GPU_MAX_HW_QUEUES for this process, set before HIP starts (-1: 8 unless the environment "
+                         "sets it; 0: leave the environment): the library runs one render stream fewer than "
+                         "this, 2..4 (rt_host.cpp pipeline_env)")
+    ap.add_argument("--output", default="f32", choices=["f32", "rgb8"],
+                    help="f32: the linear frame (12 B/pixel gathered); rgb8: gamma/u8 epilogue on every rank "
+                         "before the gather (3 B/pixel), the reference's output format")
+    ap.add_argument("--corrected-steps", type=int, default=5,
+                    help="frames of the same workload with the corrected camera, reported as corrected_camera "
+                         "(0: skip)")
     ap.add_argument("--rehearse-gather", action="store_true",
                     help="with --rehearse-world N: stand in for rank 0's gather with its device work on the "
                          "caller stream (the N-1 peer tiles copied into the gather buffer, then the "
@@ -82,17 +94,28 @@ def parse():
     return ap.parse_args()
 
 
+def lib_sha256():
+    """sha256 of the product library this process loads: PMC summaries are stamped with it."""
+    import hashlib
+    from raytracinginoneweekend_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def pmc_fields(path, kernel, config):
     """HBM traffic and VALU issue of the render kernel from a committed rocprofv3 --pmc summary
-    (scripts/pmc_json.py) of the same kernel and workload; None when absent or mismatched."""
+    (scripts/pmc_json.py) of the same kernel, workload AND build (sha256 of librt_mi355x.so);
+    (record, status) with record None when absent, mismatched or from another build."""
     try:
         with open(path) as f:
             rec = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "absent"
     if rec.get("kernel") != kernel or rec.get("config") != config:
-        return None
-    return rec
+        return None, "other kernel or workload"
+    if rec.get("lib_sha256") != lib_sha256():
+        return None, "stale: summary of another build of librt_mi355x.so"
+    return rec, "current build"
 
 
 def frames_in_flight():
@@ -104,62 +127,94 @@ def frames_in_flight():
     return max(2, min(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) - 1, 4))
 
 
+def cpu_info():
+    """(model, nproc, affinity cores, cores this job may use): the GPU box gives one GPU's job
+    a share of the host (OMP_NUM_THREADS, 16 there) out of a larger affinity set."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return model, nproc, aff, max(1, min(aff, share))
+
+
 def cpu_baseline(cfg, camera, seed, rows, threads):
-    """Reference CPU path (oracle/_ref/ref_harness_pcg) on `rows` evenly spaced rows."""
+    """The CPU baseline of BASELINE.md §4 on this host, on evenly spaced rows of the frame:
+    - value: the REFERENCE's own CPU path (oracle/_ref/ref_harness_pcg, compiled from
+      /root/reference: per-call std::vector + stable_partition + min_element,
+      raytracer.hxx:100-117) on every core this job may use, rows interleaved over threads;
+    - single_thread: the same binary on one thread (a smaller row sample);
+    - optimized: the CPU restatement (oracle/rt_oracle.cpp: allocation-free closest hit, the
+      same bits) on the same cores and rows."""
     scene, W, H, spp, depth = cfg
+    model, nproc, aff, share = cpu_info()
+    threads = threads or share
     step = max(1, H // rows)
     nrows = min(rows, (H + step - 1) // step)
-    threads = threads or int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
-    exe = os.path.join(REPO, "oracle", "_ref", "ref_harness_pcg")
-    sample = f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, {scene} scene, {camera} camera"
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_binding as O
+    import raytracinginoneweekend_amd as rt
+    host = {"cores": threads, "nproc": nproc, "affinity_cores": aff, "model": model}
     if scene == "cuda":  # the CUDA variant has no CPU path in the reference: the restatement
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        import oracle_binding as O
-        import raytracinginoneweekend_amd as rt
         s, m = rt.cuda_scene_arrays()
         p = O.make_params(W, H, spp, depth, 0, 0, step, nrows, flags=rt.abi.RT_FLAG_CUDA_COMPAT)
         t0 = time.perf_counter()
         O.render_cuda_compat(s, m, rt.Camera.cuda(W, H).c, p, threads=threads)
         sec = time.perf_counter() - t0
-        return {"value": round(W * nrows * spp / sec / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
-                "sample": f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, cuda_impl preset; {sec:.1f} s wall"}
-    if os.path.exists(exe):
+        return dict(value=round(W * nrows * spp / sec / 1e6, 4), unit="Mrays/s", kind="port",
+                    sample=f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, cuda_impl preset; {sec:.1f} s wall",
+                    **host)
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_harness_pcg")
+    if not os.path.exists(exe):
+        raise SystemExit(f"cpu_baseline: {exe} is not built (oracle/build_ref.sh)")
+
+    def ref_run(row_step, n, thr):
         cmd = [exe, "--scene", scene, "--scene-seed", "1234", "--w", str(W), "--h", str(H), "--spp", str(spp),
                "--depth", str(depth), "--seed", str(seed), "--camera", camera, "--row0", "0",
-               "--row-step", str(step), "--rows", str(nrows), "--threads", str(threads), "--time"]
+               "--row-step", str(row_step), "--rows", str(n), "--threads", str(thr), "--time"]
         out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
-        r = json.loads(out.strip().splitlines()[-1])
-        return {"value": round(r["mrays_per_s"], 4), "unit": "Mrays/s", "cores": threads, "kind": "reference",
-                "sample": sample + f"; {r['seconds']:.1f} s wall"}
-    # fallback: the CPU restatement (bit-identical to the reference, tests/test_oracle_golden.py)
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import numpy as np
-    import oracle_binding as O
-    import raytracinginoneweekend_amd as rt
+        return json.loads(out.strip().splitlines()[-1])
+
+    r = ref_run(step, nrows, threads)
+    n1 = max(1, nrows // 16)
+    s1 = max(1, H // n1)
+    r1 = ref_run(s1, n1, 1)
     s, m = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
     cam = O.camera_default(W, H, 1 if camera == "corrected" else 0)
     p = O.make_params(W, H, spp, depth, seed, 0, step, nrows)
     t0 = time.perf_counter()
     O.render_f32(s, m, cam, p, threads=threads)
-    sec = time.perf_counter() - t0
-    del np
-    return {"value": round(W * nrows * spp / sec / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": sample + f"; {sec:.1f} s wall"}
+    so = time.perf_counter() - t0
+    return dict(
+        value=round(r["mrays_per_s"], 4), unit="Mrays/s", kind="reference",
+        sample=f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, {scene} scene, {camera} camera; "
+               f"{r['seconds']:.1f} s wall; the rows' rate stands for the frame's (linear in rows)",
+        single_thread={"value": round(r1["mrays_per_s"], 4), "cores": 1, "kind": "reference",
+                       "sample": f"{n1} rows (every {s1}th); {r1['seconds']:.1f} s wall"},
+        optimized={"value": round(W * nrows * spp / so / 1e6, 4), "cores": threads, "kind": "port",
+                   "sample": f"same rows, the restatement oracle/rt_oracle.cpp; {so:.1f} s wall"},
+        **host)
 
 
 def main():
     args = parse()
-    if args.hw_queues > 0:  # before anything starts HIP
-        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
+    if args.hw_queues > 0 or (args.hw_queues < 0 and not os.environ.get("GPU_MAX_HW_QUEUES")):
+        # before anything starts HIP: 8 queues -> 4 render streams unless the caller chose
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues if args.hw_queues > 0 else 8)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    if world != args.gpus and world == 1:
+        raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
     distributed = world > 1
     torch.cuda.set_device(local)
     if distributed:
@@ -171,8 +226,6 @@ def main():
     arrays = rt.huge_scene_arrays(1234) if scene_name == "huge" else (
         rt.cuda_scene_arrays() if compat else rt.simple_scene_arrays())
     n_spheres = len(arrays[0])
-    mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
-    cam = rt.Camera.cuda(W, H) if compat else rt.Camera.default(W, H, mode)
     from raytracinginoneweekend_amd.rowtiles import FrameGather, rank_params
     rehearse = args.rehearse_world if world == 1 and args.rehearse_world > 1 else 0
     params = rank_params(W, H, spp, rehearse or world, rank, max_depth=depth, seed=args.seed,
@@ -182,7 +235,9 @@ def main():
     dev = torch.device("cuda", local)
     ds = rt.DeviceScene(arrays, device=local)
     tile = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
-    gather = FrameGather(tile, world, rank)
+    rgb8 = args.output == "rgb8"
+    tile8 = torch.empty((rows, W, 3), dtype=torch.uint8, device=dev) if rgb8 else None
+    gather = FrameGather(tile8 if rgb8 else tile, world, rank)
     seg = torch.zeros(3, dtype=torch.int64, device=dev)  # segments, sphere tests, box tests
     stream = torch.cuda.current_stream(dev)
 
@@ -190,79 +245,98 @@ def main():
         fake = torch.empty((rehearse, rows, W, 3), dtype=torch.float32, device=dev)
         frame_r = torch.empty((rows * rehearse, W, 3), dtype=torch.float32, device=dev)
 
-    def step(count_segments):
-        ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
-        if not rehearse:
-            gather(tile)
-        elif args.rehearse_gather:
-            for r in range(1, rehearse):  # one copy kernel per peer, as the gather's receives
-                fake[r].copy_(tile)
-            frame_r.view(rows, rehearse, W, 3).copy_(fake.transpose(0, 1))
+    def measure(cam, steps, warmup):
+        """warmup untimed frames, then `steps` frames timed between barriers + syncs (max over
+        ranks), then one frame alone three times (its latency, median); segment counters of
+        the timed frames."""
+        def step(count_segments):
+            ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
+            if rgb8:
+                rt.epilogue_rgb8_device(tile.data_ptr(), tile8.data_ptr(), rows * W, stream.cuda_stream)
+            if not rehearse:
+                gather(tile8 if rgb8 else tile)
+            elif args.rehearse_gather:
+                for r in range(1, rehearse):  # one copy kernel per peer, as the gather's receives
+                    fake[r].copy_(tile)
+                frame_r.view(rows, rehearse, W, 3).copy_(fake.transpose(0, 1))
 
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    seg.zero_()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kt = ds.kernel_times(args.steps)  # render-kernel durations of the timed steps (HIP events)
-    # one frame alone (no frame in flight beside it): its latency, median of 3
-    lat = []
-    for _ in range(3):
+        for _ in range(warmup):
+            step(False)
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
-        t1 = time.perf_counter()
-        step(False)
         torch.cuda.synchronize()
-        lat.append(time.perf_counter() - t1)
-    latency = sorted(lat)[1]
-    if distributed:
-        t = torch.tensor([latency], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        latency = float(t.item())
-    segments, sph_tests, box_tests = [int(x) for x in seg.tolist()]
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        sg = seg.clone()
-        dist.all_reduce(sg)
-        segments_all = int(sg[0].item())
-    else:
-        segments_all = segments
+        seg.zero_()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(True)
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        spans = ds.kernel_times(steps)  # HIP-event spans of the timed frames' render launches
+        lat = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            if distributed:
+                dist.barrier()
+            t1 = time.perf_counter()
+            step(False)
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t1)
+        latency = sorted(lat)[1]
+        counts = [int(x) for x in seg.tolist()]
+        counts_all = counts
+        if distributed:
+            t = torch.tensor([elapsed, latency], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, latency = float(t[0].item()), float(t[1].item())
+            sg = seg.clone()
+            dist.all_reduce(sg)
+            counts_all = [int(x) for x in sg.tolist()]
+        return elapsed, latency, spans, counts, counts_all
 
-    primaries = W * rows * spp * args.steps if rehearse else W * H * spp * args.steps
-    value = primaries / elapsed / 1e6
-    # roofline of the dominant kernel (render_kernel) on this rank
-    k_avg_ms = sum(kt) / len(kt)
-    # executed work: every ray-sphere test the kernel ran (20 FLOP) + every cluster AABB test
-    # (19 FLOP); brute force executes segments x n_spheres tests
-    flop_per_launch = (sph_tests * FLOP_PER_TEST + box_tests * FLOP_PER_BOX) / args.steps
-    achieved = flop_per_launch / (k_avg_ms * 1e-3) / 1e12
-    # consecutive launches overlap (frames in flight, half grids while others run), so a
-    # launch's own duration is longer than its share of the GPU: the same work per frame over
-    # the steady-state frame period is the throughput view
-    achieved_stream = flop_per_launch / (elapsed / args.steps) / 1e12
-    brute_equiv = segments / args.steps * n_spheres * FLOP_PER_TEST / (k_avg_ms * 1e-3) / 1e12
+    def summary(elapsed, latency, spans, counts, counts_all, steps):
+        segments, sph_tests, box_tests = counts
+        primaries = (W * rows if rehearse else W * H) * spp * steps
+        period = elapsed / steps
+        # executed work per frame on this rank: every ray-sphere test (20 FLOP, SURVEY §8d)
+        # and every cluster-box slab test (19 FLOP, DESIGN §6) the kernel ran
+        flop_frame = (sph_tests * FLOP_PER_TEST + box_tests * FLOP_PER_BOX) / steps
+        achieved = flop_frame / period / 1e12
+        span = sum(spans) / max(len(spans), 1)
+        return {
+            "value": primaries / elapsed / 1e6, "ms_per_step": period * 1e3, "frame_latency_ms": latency * 1e3,
+            "segments_per_primary": counts_all[0] / primaries,
+            "msegments_per_s": counts_all[0] / elapsed / 1e6,
+            "gtests_per_s": counts_all[1] / elapsed / 1e9, "gbox_tests_per_s": counts_all[2] / elapsed / 1e9,
+            "tests_per_segment": sph_tests / max(segments, 1), "boxes_per_segment": box_tests / max(segments, 1),
+            "flop_per_frame": flop_frame, "achieved": achieved,
+            # the reference's brute force: every segment tests every sphere
+            "effective_tflops": segments / steps * n_spheres * FLOP_PER_TEST / period / 1e12,
+            "span_ms": span, "span_achieved": flop_frame / (span * 1e-3) / 1e12 if span else None,
+        }
+
+    mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
+    cam = rt.Camera.cuda(W, H) if compat else rt.Camera.default(W, H, mode)
+    main_m = summary(*measure(cam, args.steps, args.warmup), args.steps)
+    corr = None
+    if args.corrected_steps > 0 and not compat and args.camera == "reference":
+        # the representative path-tracing load (7 segments per primary): the corrected camera
+        # (direction - origin) on the same workload, a few frames after the headline ones
+        corr = summary(*measure(rt.Camera.default(W, H, rt.CORRECTED), args.corrected_steps, 1),
+                       args.corrected_steps)
     if rank == 0:
+        r3 = lambda x: round(x, 3) if x is not None else None  # noqa: E731
         rec = {
             "metric": "Mrays/sec + frame wall-clock, huge-scene 1280x720x128spp @1/2/4/8 GPU",
-            "value": round(value, 3),
+            "value": round(main_m["value"], 3),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": r3(main_m["ms_per_step"]),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -272,39 +346,61 @@ def main():
                        "width": W, "height": H, "spp": spp, "max_depth": depth, "camera": args.camera,
                        "kernel": "compat_kernel (cuda_impl.cu semantics, bit-exact vs its restatement)" if compat else
                        ("fast (FMA, stated tolerance)" if args.variant == "fast" else f"{args.variant} (bit-exact)")
-                       + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather",
-                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
-            "frame_wall_ms": round(elapsed / args.steps * 1e3, 3),
-            "frame_latency_ms": round(latency * 1e3, 3),
+                       + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather of "
+                       + ("u8 (gamma epilogue per rank)" if rgb8 else "f32") + " tiles",
+                       "output": args.output, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
+            # ms_per_step is the steady-state period of a frame stream (frames in flight);
+            # frame_wall_ms is ONE frame alone, start to finish (render, accumulate, gather)
+            "frame_wall_ms": r3(main_m["frame_latency_ms"]),
+            "frame_latency_ms": r3(main_m["frame_latency_ms"]),
             "frames_in_flight": frames_in_flight(),
-            "segments_per_primary": round(segments_all / primaries, 4),
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                         "kernel": "compat_kernel" if compat else "render_kernel", "kernel_avg_ms": round(k_avg_ms, 3),
-                         "flop_per_launch": flop_per_launch, "work": "executed sphere+box tests",
-                         "brute_force_equiv_tflops": round(brute_equiv, 2),
-                         "achieved_frame_stream": round(achieved_stream, 3),
-                         "frac_frame_stream": round(achieved_stream / PEAK_FP32_TFLOPS, 4)},
-            "tests_per_segment": round(sph_tests / max(segments, 1), 2),
-            "kernel_tests_per_s": round(sph_tests / args.steps / (k_avg_ms * 1e-3) / 1e12, 4),
-            "boxes_per_segment": round(box_tests / max(segments, 1), 2),
+            "segments_per_primary": round(main_m["segments_per_primary"], 4),
+            "msegments_per_s": round(main_m["msegments_per_s"], 1),
+            "gtests_per_s": round(main_m["gtests_per_s"], 2),
+            "gbox_tests_per_s": round(main_m["gbox_tests_per_s"], 2),
+            "tests_per_segment": round(main_m["tests_per_segment"], 2),
+            "boxes_per_segment": round(main_m["boxes_per_segment"], 2),
+            "roofline": {
+                "bound": "valu", "achieved": r3(main_m["achieved"]), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(main_m["achieved"] / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                "kernel": "compat_kernel" if compat else "render_kernel",
+                "work": "executed ray-sphere tests x 20 FLOP + cluster-box tests x 19 FLOP per frame, over the "
+                        "frame period (ms_per_step)",
+                "flop_per_frame": main_m["flop_per_frame"],
+                "frac_unpacked": round(main_m["achieved"] / PEAK_FP32_TFLOPS * 2, 4),
+                # brute-force equivalent (segments x spheres x 20 FLOP over the period): a speed-up
+                # figure over the reference's algorithm, NOT a fraction of any peak
+                "effective_tflops": round(main_m["effective_tflops"], 2),
+                # a frame's render launches overlap other frames' (frames in flight): their
+                # HIP-event span is a latency, shown for reference only
+                "per_launch_span_ms": r3(main_m["span_ms"]),
+                "per_launch_span_achieved": r3(main_m["span_achieved"]),
+            },
         }
         v = {"exact": 0, "scalar": 1, "fast": 2}[args.variant]
         cull = 0 if args.traversal == "brute" or v == 1 else 7
         kname = f"render_kernel<{v}, {cull}, false>"
-        pmc = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
-                                            "traversal": args.traversal, "n_gpus": world})
+        pmc, status = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
+                                                   "traversal": args.traversal, "n_gpus": world})
+        rec["roofline"]["pmc_status"] = status
         if pmc and not rehearse:
-            # HBM bytes per launch (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE) and
-            # the VALU issue fraction, from the committed PMC summary of this kernel
+            # HBM bytes per frame (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, one
+            # launch per frame here) and the VALU issue, from the PMC summary of THIS build
             rec["roofline"]["traffic"] = pmc["hbm_bytes_per_launch"]
-            rec["roofline"]["traffic_unit"] = "bytes/launch"
-            rec["roofline"]["valu_busy"] = pmc["valu_busy"]
-            # the same VALU instructions per frame over the steady-state frame period (launches
-            # overlap there; valu_busy above divides by one serialized dispatch's duration)
-            rec["roofline"]["valu_busy_frame_stream"] = round(
-                pmc["valu_insts"] * 2.0 / (1024 * pmc["clock_ghz"] * 1e9 * elapsed / args.steps), 4)
+            rec["roofline"]["traffic_unit"] = "bytes/frame"
+            rec["roofline"]["valu_insts_per_frame"] = pmc["valu_insts"]
+            # VALU pipe busy over the frame period: wave64 VALU = 2 cycles, 1024 SIMDs
+            rec["roofline"]["valu_busy"] = round(
+                pmc["valu_insts"] * 2.0 / (1024 * pmc["clock_ghz"] * 1e9 * main_m["ms_per_step"] * 1e-3), 4)
             rec["roofline"]["pmc_source"] = os.path.relpath(args.pmc, REPO)
+        if corr:
+            rec["corrected_camera"] = {
+                "value": round(corr["value"], 3), "unit": "Mrays/s", "steps": args.corrected_steps,
+                "ms_per_step": r3(corr["ms_per_step"]), "frame_latency_ms": r3(corr["frame_latency_ms"]),
+                "segments_per_primary": round(corr["segments_per_primary"], 4),
+                "msegments_per_s": round(corr["msegments_per_s"], 1), "gtests_per_s": round(corr["gtests_per_s"], 2),
+                "roofline_achieved": r3(corr["achieved"]), "roofline_frac": round(corr["achieved"] / PEAK_FP32_TFLOPS, 4),
+                "effective_tflops": round(corr["effective_tflops"], 2)}
         if rehearse:
             rec["rehearsal"] = (f"rank 0 of {rehearse}: rows 0, {rehearse}, ... ({rows} rows), "
                                 + ("gather's device copies stood in on the caller stream" if args.rehearse_gather

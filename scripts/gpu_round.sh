@@ -23,7 +23,7 @@ for s in ${STEPS:-smoke pytest bench prof}; do
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     ab)     step ab 900 python scripts/ab_variants.py --rounds ${AB_ROUNDS:-5} --variants ${AB_VARIANTS:-exact:cull,fast:cull} ;;
     abl)    RT_LIB_PATH=$PWD/scripts/_abl/librt_mi355x.so step abl 900 python scripts/ab_variants.py --rounds ${AB_ROUNDS:-5} --variants ${AB_VARIANTS:-exact:cull,fast:cull} ;;
-    prof)   step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    prof)   step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --corrected-steps 0 ${BENCH_ARGS:-} ;;
   esac
 done
 echo "=== done"

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --corrected-steps 0}
 i=0
 while read -r line; do
   [ -z "$line" ] && continue

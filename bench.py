@@ -75,10 +75,10 @@ def parse():
     ap.add_argument("--rehearse-world", type=int, default=0,
                     help="diagnostic, 1 GPU: render only rank 0's rows of an N-way split (no gather) to "
                          "estimate one rank's frame time at N GPUs; not a bench line")
-    ap.add_argument("--hw-queues", type=int, default=-1,
-                    help="GPU_MAX_HW_QUEUES for this process, set before HIP starts (-1: 8 unless the environment "
-                         "sets it; 0: leave the environment): the library runs one render stream fewer than "
-                         "this, 2..4 (rt_host.cpp pipeline_env)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process, set before HIP starts (0: leave the environment, "
+                         "HIP's default 4): the library runs one render stream fewer than this, 2..4 "
+                         "(rt_host.cpp pipeline_env); the line records both values")
     ap.add_argument("--output", default="f32", choices=["f32", "rgb8"],
                     help="f32: the linear frame (12 B/pixel gathered); rgb8: gamma/u8 epilogue on every rank "
                          "before the gather (3 B/pixel), the reference's output format")
@@ -204,9 +204,9 @@ def cpu_baseline(cfg, camera, seed, rows, threads):
 
 def main():
     args = parse()
-    if args.hw_queues > 0 or (args.hw_queues < 0 and not os.environ.get("GPU_MAX_HW_QUEUES")):
-        # before anything starts HIP: 8 queues -> 4 render streams unless the caller chose
-        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues if args.hw_queues > 0 else 8)
+    hw_env = os.environ.get("GPU_MAX_HW_QUEUES")
+    if args.hw_queues > 0:  # before anything starts HIP: 8 queues -> 4 render streams
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import torch.distributed as dist
 
@@ -348,7 +348,8 @@ def main():
                        ("fast (FMA, stated tolerance)" if args.variant == "fast" else f"{args.variant} (bit-exact)")
                        + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather of "
                        + ("u8 (gamma epilogue per rank)" if rgb8 else "f32") + " tiles",
-                       "output": args.output, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
+                       "output": args.output, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "hw_queues_env": hw_env},
             # ms_per_step is the steady-state period of a frame stream (frames in flight);
             # frame_wall_ms is ONE frame alone, start to finish (render, accumulate, gather)
             "frame_wall_ms": r3(main_m["frame_latency_ms"]),

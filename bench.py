@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--output", default="f32", choices=["f32", "rgb8"],
                     help="f32: the linear frame (12 B/pixel gathered); rgb8: gamma/u8 epilogue on every rank "
                          "before the gather (3 B/pixel), the reference's output format")
+    ap.add_argument("--digest", action="store_true",
+                    help="add frame_sha256, the sha256 of the last frame's bytes on rank 0 (A/B bit checks)")
     ap.add_argument("--corrected-steps", type=int, default=5,
                     help="frames of the same workload with the corrected camera, reported as corrected_camera "
                          "(0: skip)")
@@ -321,6 +323,12 @@ def main():
     mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
     cam = rt.Camera.cuda(W, H) if compat else rt.Camera.default(W, H, mode)
     main_m = summary(*measure(cam, args.steps, args.warmup), args.steps)
+    digest = None
+    if args.digest and rank == 0:
+        import hashlib
+        torch.cuda.synchronize()
+        frame = gather.frame if (world > 1 and not rehearse) else (tile8 if rgb8 else tile)
+        digest = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()
     corr = None
     if args.corrected_steps > 0 and not compat and args.camera == "reference":
         # the representative path-tracing load (7 segments per primary): the corrected camera
@@ -394,6 +402,8 @@ def main():
             rec["roofline"]["valu_busy"] = round(
                 pmc["valu_insts"] * 2.0 / (1024 * pmc["clock_ghz"] * 1e9 * main_m["ms_per_step"] * 1e-3), 4)
             rec["roofline"]["pmc_source"] = os.path.relpath(args.pmc, REPO)
+        if digest:
+            rec["frame_sha256"] = digest
         if corr:
             rec["corrected_camera"] = {
                 "value": round(corr["value"], 3), "unit": "Mrays/s", "steps": args.corrected_steps,

@@ -36,6 +36,8 @@ struct FrameConsts {
     uint32_t row_offset, row_stride, tiled_rows, tiles_x, n_pixels, sample_begin;
     UDiv div_W, div_tiles_x, div_n_pixels;
     uint32_t tile_lw;  // log2 of the tile width (3..6): tiles of 2^lw x 64/2^lw pixels
+    float rW, rH;       // RN(1 / width), RN(1 / height)
+    uint32_t div_fast;  // bit 0 / 1: x / width, x / height by rW / rH + one FMA correction is exact
 };
 
 struct KParams {

@@ -16,6 +16,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -582,6 +584,35 @@ rt::UDiv make_udiv(uint32_t d)
     return r;
 }
 
+// Whether RN(a / b) == fma(fma(-q0, b, a), rb, q0) with rb = RN(1 / b), q0 = RN(a rb) for every
+// a = m (m in [2^23, 2^24), i.e. every float mantissa). Powers of two scale every step exactly,
+// so the identity then holds for every a >= 0 whose quotient and remainder stay normal: the
+// kernel's x / width and x / height (x = 0, a pixel index, or a canonical draw >= 2^-32) use
+// the two-FMA form when it holds. Checked once per divisor value (about 8 M host FMAs).
+bool exact_by_reciprocal(float b)
+{
+    static std::mutex mu;
+    static std::map<uint32_t, bool> cache;
+    uint32_t key;
+    std::memcpy(&key, &b, 4);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    bool ok = std::isfinite(b) && b > 0.f && b >= 0x1p-60f && b <= 0x1p60f;
+    const float rb = 1.f / b;
+    for (uint32_t m = 1u << 23; ok && m < (1u << 24); ++m) {
+        const float a = static_cast<float>(m);
+        const float q0 = a * rb;
+        const float q = std::fma(std::fma(-q0, b, a), rb, q0);
+        ok = q == a / b;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = ok;
+    return ok;
+}
+
 void fill_frame_consts(rt::KParams &k)
 {
     rt::FrameConsts &f = k.fc;
@@ -606,6 +637,9 @@ void fill_frame_consts(rt::KParams &k)
     f.div_W = make_udiv(k.W);
     f.div_tiles_x = make_udiv(k.tiles_x);
     f.div_n_pixels = make_udiv(k.n_pixels);
+    f.rW = 1.f / f.fW;
+    f.rH = 1.f / f.fH;
+    f.div_fast = (exact_by_reciprocal(f.fW) ? 1u : 0u) | (exact_by_reciprocal(f.fH) ? 2u : 0u);
 }
 
 // A passing cluster requested by at most RT_TRANSPOSE_MAX lanes (default 16, at most 16; 0 =

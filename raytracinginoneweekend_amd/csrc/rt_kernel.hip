@@ -69,10 +69,31 @@ __device__ __forceinline__ uint64_t pcg_seed(uint64_t initstate, uint64_t inc)
     return st * 6364136223846793005ULL + inc;
 }
 // libstdc++ generate_canonical<float,24> over a 32-bit engine: float(x) / 2^32, kept < 1.
+// float(x) rounds up to 2^32 for the top 128 words; clamping it to the largest float below,
+// 2^32 - 256, before the exact scaling gives the same 0x1.fffffep-1.
 __device__ __forceinline__ float canonical(uint64_t &st, uint64_t inc)
 {
-    float r = (float)pcg_next(st, inc) * 0x1p-32f;
-    return r >= 1.f ? 0x1.fffffep-1f : r;
+    return fminf((float)pcg_next(st, inc), 0x1.fffffep31f) * 0x1p-32f;
+}
+// canonical() * 2.f + -1.f (raytracer.hxx:35-37): the product is exact, so the result is the
+// one rounding of clamp(float(x)) * 2^-31 - 1, i.e. a single FMA.
+__device__ __forceinline__ float canonical_pm1(uint64_t &st, uint64_t inc)
+{
+    return fmaf(fminf((float)pcg_next(st, inc), 0x1.fffffep31f), 0x1p-31f, -1.f);
+}
+// RN(a / b) for a per-render divisor b (the image width or height): one reciprocal rb = RN(1/b)
+// and one FMA correction (Markstein) when the host has checked, for this b, that the sequence
+// reproduces the IEEE quotient for every float mantissa (rt_host.cpp exact_by_reciprocal: the
+// result then holds for every normal a >= 0, the scaling by powers of two being exact);
+// otherwise the IEEE division.
+__device__ __forceinline__ float div_const(float a, float b, float rb, bool fast)
+{
+    if (fast) {
+        const float q0 = a * rb;
+        const float r = fmaf(-q0, b, a);
+        return fmaf(r, rb, q0);
+    }
+    return a / b;
 }
 // raytracer.hxx:32-43. `length(p) > 1` is evaluated as `norm(p) > 1 + 2^-23`: with a
 // correctly rounded sqrt the two agree for every non-negative float (checked exhaustively,
@@ -81,9 +102,9 @@ __device__ __forceinline__ f3 random_in_unit_sphere(uint64_t &st, uint64_t inc)
 {
     f3 p;
     do {
-        float x = canonical(st, inc) * 2.f + -1.f;
-        float y = canonical(st, inc) * 2.f + -1.f;
-        float z = canonical(st, inc) * 2.f + -1.f;
+        float x = canonical_pm1(st, inc);
+        float y = canonical_pm1(st, inc);
+        float z = canonical_pm1(st, inc);
         p = mk(x, y, z);
     } while (p.x * p.x + p.y * p.y + p.z * p.z > 0x1.000002p+0f);
     return p;
@@ -104,9 +125,9 @@ __device__ __forceinline__ f3 random_in_unit_sphere_capped(uint64_t &st, uint64_
     f3 p = mk(0.f, 0.f, 0.f);
     got = false;
     for (int k = 0; k < (RT_REJECT_CAP > 0 ? RT_REJECT_CAP : 1); ++k) {
-        const float x = canonical(st, inc) * 2.f + -1.f;
-        const float y = canonical(st, inc) * 2.f + -1.f;
-        const float z = canonical(st, inc) * 2.f + -1.f;
+        const float x = canonical_pm1(st, inc);
+        const float y = canonical_pm1(st, inc);
+        const float z = canonical_pm1(st, inc);
         if (!(x * x + y * y + z * z > 0x1.000002p+0f)) {
             p = mk(x, y, z);
             got = true;
@@ -180,6 +201,14 @@ struct Hit {
     float t;
     uint32_t id;   // original sphere index, 0xffffffff = none
 };
+
+// Work counters of one wave (wave-uniform, scalar registers): segments traced and the
+// lane-level ray-sphere and cluster-box tests executed, summed from ballots in uniform control
+// flow (a test the wave runs for k requesting lanes counts k).
+struct WaveTally {
+    uint64_t seg, sph, box;
+};
+__device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(__ballot(x)); }
 
 template <bool FAST, bool STATS, int N = 8>
 __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx, uint32_t i,
@@ -373,13 +402,13 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
 template <bool FAST, bool STATS>
 __device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, const float4 *__restrict__ geo,
                                                  const uint32_t *__restrict__ sidx, TransposeLds *tw, uint32_t tmax,
-                                                 f3 o, f3 d, float a, Hit &h, Dbg &dbg, uint32_t &tests)
+                                                 f3 o, f3 d, float a, Hit &h, Dbg &dbg, WaveTally &wt)
 {
     const uint64_t M = __ballot(req);
     if (!M) return;
     const uint32_t scu = __builtin_amdgcn_readfirstlane(scu_lane);
     const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-    if (req) tests += cnt << 16;
+    wt.sph += (uint64_t)__popcll(M) * cnt;
     if ((uint32_t)__popcll(M) <= tmax && cnt <= 16u) {
         members_transposed<FAST>(geo, sidx, start, cnt, M, req, tw, o, d, a, h);
     } else if (req) {
@@ -391,12 +420,11 @@ __device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, co
 template <bool FAST, int CULL, bool STATS>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
-                                           f3 d, Dbg &dbg, uint32_t &tests, bool active, TransposeLds *tw)
+                                           f3 d, Dbg &dbg, WaveTally &wt, bool active, TransposeLds *tw)
 {
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
     Hit h{RT_TMAX, 0xffffffffu};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, a, h, dbg);
-    tests += p.n_always;
     if (CULL) {
         auto safe_rcp = [](float x) {
             return __builtin_amdgcn_rcpf(fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x);
@@ -416,25 +444,26 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float4 *sup = clus + (p.supers_offset - p.clus_offset);
         uint32_t n_supers = p.n_supers;
         if (p.use_root) {
-            tests += active ? 1u : 0u;
+            wt.box += lanes(active);
             if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t * 1.002f)))
                 n_supers = 0;
         }
         for (uint32_t g = 0; g < n_supers; ++g) {
             const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
-            tests += active ? 1u : 0u;
+            wt.box += lanes(active);
             const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t * 1.002f);
-            if (!__ballot(sp)) continue;
+            const uint64_t spm = __ballot(sp);
+            if (!spm) continue;
             const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
-            tests += sp ? 4u : 0u;
+            wt.box += 4u * (uint32_t)__popcll(spm);
             for (uint32_t c = c0i; c < c0i + 4; c += 2) {
                 const float tb_now = h.t * 1.002f;
                 const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
                 const bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
                 cluster_members7<FAST, STATS>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
-                                              dbg, tests);
+                                              dbg, wt);
                 cluster_members7<FAST, STATS>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
-                                              dbg, tests);
+                                              dbg, wt);
             }
         }
     }
@@ -484,6 +513,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         __shared__ TransposeLds s_tw[4];
         tw = &s_tw[threadIdx.x >> 6];
     }
+    __shared__ float4 lds_pn[256];  // per lane: a pending metal scatter's normal and roughness
 
     // wave-uniform cursor over the item space
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
@@ -497,13 +527,13 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     uint32_t depth = 0;
     uint64_t rng = 0;
     // a lambert/metal hit leaves its scatter offset to the next iteration's rejection loop:
-    // o = hit point; d = p + n (lambert) or reflect(unit(d), n) (metal); pn = n, roughness
+    // o = hit point; d = p + n (lambert) or reflect(unit(d), n) (metal); the metal's normal and
+    // roughness wait in the lane's LDS word (pn: 16 B per lane, no registers held across the loop)
     bool pend = false, pend_metal = false;
     // a fresh sample whose lens draw did not finish within RT_REJECT_CAP attempts: its camera
     // stream state waits in (o.x, o.y) and its jittered (u, v) in (d.x, d.y) until it does
     bool pend_lens = false;
-    float4 pn = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint32_t segs = 0, tests_sph = 0, tests_box = 0;  // per-lane tallies (widened at the end)
+    WaveTally wt{0, 0, 0};
     Dbg dbg{0, 0, 0, 0, 0};
     uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0;
     uint64_t t_dry = 0;  // STATS: realtime when this wave found every queue empty
@@ -521,6 +551,26 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
 
     for (;;) {
         stamp(4);
+#ifdef RT_EXTRA_VALU  // timing probe only (scripts/build_variant.sh): RT_EXTRA_VALU more VALU per wave iteration
+        {
+            float e0 = o.x, e1 = o.y, e2 = o.z, e3 = d.x;
+            asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2), "+v"(e3));
+#pragma unroll
+            for (int k = 0; k < RT_EXTRA_VALU / 4; ++k) {
+                e0 = fmaf(e0, 1.0001f, 0.5f); e1 = fmaf(e1, 1.0001f, 0.5f);
+                e2 = fmaf(e2, 1.0001f, 0.5f); e3 = fmaf(e3, 1.0001f, 0.5f);
+            }
+            asm volatile("" ::"v"(e0), "v"(e1), "v"(e2), "v"(e3));
+        }
+#endif
+#ifdef RT_EXTRA_SALU  // timing probe only: RT_EXTRA_SALU more SALU per wave iteration
+        {
+            uint32_t s0 = __builtin_amdgcn_readfirstlane(pix);
+#pragma unroll
+            for (int k = 0; k < RT_EXTRA_SALU; ++k) asm volatile("s_add_u32 %0, %0, 3" : "+s"(s0));
+            asm volatile("" ::"s"(s0));
+        }
+#endif
         fc_ptr_t fc = fc_base;
         asm volatile("" : "+s"(fc));
         // ---- refill items for idle lanes and start their samples -------------------
@@ -601,11 +651,12 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             const uint64_t inc_cam = ((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo;
             rng = pcg_seed(key, inc_data);
             rc = pcg_seed(key, inc_cam);
-            const float fW = fc->fW, fH = fc->fH;
-            const float u = (float)px / fW;
-            const float v = (float)py / fH;
-            uu = u + canonical(rng, inc_data) / fW;
-            vv = v + canonical(rng, inc_data) / fH;
+            const float fW = fc->fW, fH = fc->fH, rW = fc->rW, rH = fc->rH;
+            const bool fw = fc->div_fast & 1u, fh = fc->div_fast & 2u;
+            const float u = div_const((float)px, fW, rW, fw);
+            const float v = div_const((float)py, fH, rH, fh);
+            uu = u + div_const(canonical(rng, inc_data), fW, rW, fw);
+            vv = v + div_const(canonical(rng, inc_data), fH, rH, fh);
             att = mk(1.f, 1.f, 1.f);
             depth = 0;
         }
@@ -657,6 +708,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                 if (!pend_metal) {
                     d = (d + r) - o;                       // lambert :135, d held p + n, o = p
                 } else {
+                    const float4 pn = lds_pn[threadIdx.x];
                     const f3 nd = d + r * pn.w;            // metal :147, d held reflect(unit(d), n)
                     if (dot(nd, mk(pn.x, pn.y, pn.z)) > 0.f) {
                         d = nd;
@@ -684,21 +736,17 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && !defer && depth < p.max_depth;  // depth check: main.cxx:74
         Hit h{RT_TMAX, 0xffffffffu};
-        uint32_t tally = 0;  // low 16 bits: always-list spheres + box tests; high: member spheres
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
-            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, seg, tw);
-            if (!seg) {
-                h = Hit{RT_TMAX, 0xffffffffu};
-                tally = 0;
-            }
+            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, wt, seg, tw);
+            if (!seg) h = Hit{RT_TMAX, 0xffffffffu};
         } else if (seg) {
-            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, tally, true, nullptr);
+            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, wt, true, nullptr);
         }
         stamp(2);
         {
-            const uint32_t al = seg ? p.n_always : 0u;
-            tests_sph += al + (tally >> 16);
-            tests_box += (tally & 0xffffu) - al;
+            const uint32_t ns = lanes(seg);  // segments of this iteration (main.cxx:74 passed)
+            wt.seg += ns;
+            wt.sph += (uint64_t)ns * p.n_always;
         }
 
         // ---- shading: the hit of every live lane -----------------------------------------
@@ -708,7 +756,6 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             if (!seg) {
                 done = true;  // main.cxx:74 (only reachable with max_depth == 0)
             } else {
-                ++segs;
                 const float t = h.t;
                 const uint32_t ib = h.id;
                 ++depth;
@@ -753,7 +800,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                         const f3 rf = reflect(ud, hn);
                         if (kind == 1u) {                       // metal, :143-156
                             d = rf;                             // + rius * roughness next iteration
-                            pn = make_float4(hn.x, hn.y, hn.z, md.w);
+                            lds_pn[threadIdx.x] = make_float4(hn.x, hn.y, hn.z, md.w);
                             pend = true;
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
@@ -790,17 +837,15 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     if (p.segments) {
         // wave reductions, one atomic per wave and counter: [0] segments, [1] sphere tests,
         // [2] cluster box tests (lane-level, executed)
-        const unsigned long long c[3] = {segs, tests_sph, tests_box};  // widened before the reduction
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            unsigned long long v = c[i];
-            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-            if (lane == 0) atomicAdd(p.segments + i, v);
+        if (lane == 0) {  // one atomic per wave and counter
+            atomicAdd(p.segments + 0, (unsigned long long)wt.seg);
+            atomicAdd(p.segments + 1, (unsigned long long)wt.sph);
+            atomicAdd(p.segments + 2, (unsigned long long)wt.box);
         }
     }
     if (STATS && p.dbg) {
         const uint32_t c[8] = {dbg_iters, dbg_refills, dbg.wave_blocks, dbg.lane_blocks, dbg.wave_roots,
-                               dbg.lane_roots, (uint32_t)segs, dbg.wave_member_blocks};
+                               dbg.lane_roots, lane == 0 ? (uint32_t)wt.seg : 0u, dbg.wave_member_blocks};
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             unsigned long long v = c[i];

@@ -197,10 +197,12 @@ __device__ __forceinline__ bool first_active_lane()
     return (threadIdx.x & 63u) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63u);
 }
 
-struct Hit {
-    float t;
-    uint32_t id;   // original sphere index, 0xffffffff = none
+struct Hit {  // the closest candidate so far as hit_key(t, original index); ~0 = none
+    uint64_t key;
+    __device__ float t() const { return __uint_as_float((uint32_t)(key >> 32)); }
+    __device__ uint32_t id() const { return (uint32_t)key; }
 };
+constexpr uint64_t kNoHit = 0x7f7fffffffffffffull;  // t = kMAX, index = none
 
 // Work counters of one wave (wave-uniform, scalar registers): segments traced and the
 // lane-level ray-sphere and cluster-box tests executed, summed from ballots in uniform control
@@ -209,6 +211,22 @@ struct WaveTally {
     uint64_t seg, sph, box;
 };
 __device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(__ballot(x)); }
+
+// t in (kMIN, kMAX), the reference's test (raytracer.hxx:63-64,76-77): positive binary32 values
+// are ordered as their bit patterns, and as unsigned integers every negative value and every
+// NaN lies outside the open interval of patterns, so one subtract and one compare decide it.
+__device__ __forceinline__ bool in_range(float t)
+{
+    constexpr uint32_t lo = 0x3c03126fu;  // bits of RT_TMIN (0.008f)
+    constexpr uint32_t hi = 0x7f7fffffu;  // bits of RT_TMAX (FLT_MAX)
+    return __float_as_uint(t) - (lo + 1u) < hi - lo - 1u;
+}
+// A candidate as a 64-bit key, bits(t) << 32 | original index: for t > 0 (or NaN, which loses to
+// every valid t) the unsigned key order is the (t, index) order of closest_hit.
+__device__ __forceinline__ uint64_t hit_key(float t, uint32_t id)
+{
+    return ((uint64_t)__float_as_uint(t) << 32) | id;
+}
 
 template <bool FAST, bool STATS, int N = 8>
 __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx, uint32_t i,
@@ -252,15 +270,15 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
                 if (STATS) { dbg.lane_roots += pos; if (first_active_lane()) ++dbg.wave_roots; }
                 const float q = sqrtf(dq[k]);
                 float t = (-bq[k] - q) / a;                                  // :63
-                const bool ok = t < RT_TMAX && t > RT_TMIN;
+                const bool ok = in_range(t);
                 if (__ballot(pos && !ok)) {
                     const float t2 = (-bq[k] + q) / a;                       // :76
-                    t = ok ? t : (t2 < RT_TMAX && t2 > RT_TMIN ? t2 : __builtin_nanf(""));
+                    t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
                 } else {
                     t = ok ? t : __builtin_nanf("");
                 }
-                const uint32_t id = sidx[i + k];
-                if (pos && (t < h.t || (t == h.t && id < h.id))) { h.t = t; h.id = id; }
+                const uint64_t kt = hit_key(t, sidx[i + k]);
+                if (pos && kt < h.key) h.key = kt;
             }
         }
     }
@@ -292,9 +310,11 @@ __device__ __forceinline__ bool box_pass(const RayBox &r, float4 c0, float4 c1, 
 {
     const float hx = fmaf(c0.w, r.aix, r.px), hy = fmaf(c1.x, r.aiy, r.py), hz = fmaf(c1.y, r.aiz, r.pz);
     const float tcx = fmaf(c0.x, r.ix, -r.oix), tcy = fmaf(c0.y, r.iy, -r.oiy), tcz = fmaf(c0.z, r.iz, -r.oiz);
-    const float tin = fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz);
-    const float tout = fminf(fminf(tcx + hx, tcy + hy), tcz + hz);
-    return tin <= tout && tout >= t_lo && tin <= t_hi;
+    // tin <= tout && tout >= t_lo && tin <= t_hi, with t_lo < t_hi (no NaN arises: every
+    // operand is finite or an infinity of one sign)
+    const float tin = fmaxf(fmaxf(fmaxf(tcx - hx, tcy - hy), tcz - hz), t_lo);
+    const float tout = fminf(fminf(fminf(tcx + hx, tcy + hy), tcz + hz), t_hi);
+    return tin <= tout;
 }
 
 // Structure 7: the members of a passing cluster, tested transposed. A wave walks the union of
@@ -307,25 +327,28 @@ __device__ __forceinline__ bool box_pass(const RayBox &r, float4 c0, float4 c1, 
 // candidates are combined by the (t, original index) minimum as key = bits(t) << 32 | index
 // (t > 0, so the u64 order is that order): the same hit, in any order. Whole-wave code.
 constexpr uint32_t kTransposeMax = 16;  // rays per transposed cluster (KParams::transpose_max <= this)
-__device__ __forceinline__ uint64_t min16_u64(uint64_t k)  // minimum over each row of 16 lanes
+// unsigned minimum over each row of 16 lanes: xor 1, xor 2 (quad permutes), then the half-row
+// mirror and the row mirror leave every lane of a row with the row's minimum
+// (the DPP moves carry the identity of min as their old value, so the compiler folds each into
+// its v_min_u32 as a DPP operand)
+__device__ __forceinline__ uint32_t min16_u32(uint32_t v)
 {
-    uint32_t lo = (uint32_t)k, hi = (uint32_t)(k >> 32);
-    // xor 1, xor 2 (quad permutes), then half-row mirror and row mirror: every lane of a row
-    // ends with the row's minimum
-#define RT_MIN16_STEP(ctrl)                                                                     \
-    {                                                                                           \
-        const uint32_t l2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, ctrl, 0xf, 0xf, false); \
-        const uint32_t h2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, ctrl, 0xf, 0xf, false); \
-        const bool lt = h2 < hi || (h2 == hi && l2 < lo);                                       \
-        lo = lt ? l2 : lo;                                                                      \
-        hi = lt ? h2 : hi;                                                                      \
-    }
-    RT_MIN16_STEP(0xB1)
-    RT_MIN16_STEP(0x4E)
-    RT_MIN16_STEP(0x141)
-    RT_MIN16_STEP(0x140)
-#undef RT_MIN16_STEP
-    return ((uint64_t)hi << 32) | lo;
+#define RT_DPP_MIN(ctrl) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, ctrl, 0xf, 0xf, false))
+    RT_DPP_MIN(0xB1);
+    RT_DPP_MIN(0x4E);
+    RT_DPP_MIN(0x141);
+    RT_DPP_MIN(0x140);
+#undef RT_DPP_MIN
+    return v;
+}
+// minimum key over each row of 16 lanes, in two 32-bit passes: the smallest t (as bits), then the
+// smallest index among the lanes holding that t
+__device__ __forceinline__ uint64_t min16_key(uint64_t k)
+{
+    const uint32_t tb = (uint32_t)(k >> 32);
+    const uint32_t tm = min16_u32(tb);
+    const uint32_t im = min16_u32(tb == tm ? (uint32_t)k : 0xffffffffu);
+    return ((uint64_t)tm << 32) | im;
 }
 // per-wave LDS of the transposed tests: the requesting rays by rank, and each ray's minimum
 struct TransposeLds {
@@ -373,16 +396,16 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
         if (__ballot(pos)) {
             const float q = sqrtf(disc);
             float t = (-b - q) / ra;                                       // :63
-            const bool ok = t < RT_TMAX && t > RT_TMIN;
+            const bool ok = in_range(t);
             if (__ballot(pos && !ok)) {
                 const float t2 = (-b + q) / ra;                            // :76
-                t = ok ? t : (t2 < RT_TMAX && t2 > RT_TMIN ? t2 : __builtin_nanf(""));
+                t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
             } else {
                 t = ok ? t : __builtin_nanf("");
             }
-            if (pos && t == t) key = ((uint64_t)__float_as_uint(t) << 32) | sid;
+            if (pos && t == t) key = hit_key(t, sid);
         }
-        key = min16_u64(key);
+        key = min16_key(key);
         if (k == 0u && r < m) tw->key[r] = key;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -390,10 +413,7 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (req) {
         const uint64_t kk = tw->key[rank];
-        if (kk < (((uint64_t)__float_as_uint(h.t) << 32) | h.id)) {
-            h.t = __uint_as_float((uint32_t)(kk >> 32));
-            h.id = (uint32_t)kk;
-        }
+        if (kk < h.key) h.key = kk;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -423,7 +443,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
                                            f3 d, Dbg &dbg, WaveTally &wt, bool active, TransposeLds *tw)
 {
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
-    Hit h{RT_TMAX, 0xffffffffu};
+    Hit h{kNoHit};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, a, h, dbg);
     if (CULL) {
         auto safe_rcp = [](float x) {
@@ -445,19 +465,19 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         uint32_t n_supers = p.n_supers;
         if (p.use_root) {
             wt.box += lanes(active);
-            if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t * 1.002f)))
+            if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)))
                 n_supers = 0;
         }
         for (uint32_t g = 0; g < n_supers; ++g) {
             const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
             wt.box += lanes(active);
-            const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t * 1.002f);
+            const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t() * 1.002f);
             const uint64_t spm = __ballot(sp);
             if (!spm) continue;
             const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
             wt.box += 4u * (uint32_t)__popcll(spm);
             for (uint32_t c = c0i; c < c0i + 4; c += 2) {
-                const float tb_now = h.t * 1.002f;
+                const float tb_now = h.t() * 1.002f;
                 const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
                 const bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
                 cluster_members7<FAST, STATS>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
@@ -735,10 +755,10 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
 
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && !defer && depth < p.max_depth;  // depth check: main.cxx:74
-        Hit h{RT_TMAX, 0xffffffffu};
+        Hit h{kNoHit};
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
             h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, wt, seg, tw);
-            if (!seg) h = Hit{RT_TMAX, 0xffffffffu};
+            if (!seg) h = Hit{kNoHit};
         } else if (seg) {
             h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, wt, true, nullptr);
         }
@@ -756,8 +776,8 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             if (!seg) {
                 done = true;  // main.cxx:74 (only reachable with max_depth == 0)
             } else {
-                const float t = h.t;
-                const uint32_t ib = h.id;
+                const float t = h.t();
+                const uint32_t ib = h.id();
                 ++depth;
                 if (ib == 0xffffffffu) {
                     // main.cxx:71: background(.5 * unit_direction.y + 1) * attenuation

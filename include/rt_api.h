@@ -225,6 +225,14 @@ int rt_scene_debug_counters(rt_scene *scene, uint64_t out[16], int reset);
  * clock), loop iterations, and (hardware CU id << 32 | iterations after dry << 16 | refill
  * rounds); at most max_waves records, *n = records written (0 without RT_DEBUG_STATS=1).  */
 int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, uint32_t *n);
+/* Diagnostics: with RT_DEBUG_STATS=1, how often each block of the render loop ran, counted once
+ * per wave per execution, summed over the instrumented launches since the last reset: [0] loop
+ * iterations, [1] refill trips, [2] sample starts, [3] rejection attempts, [4] lens rays done,
+ * [5] scatters done, [6] root-box passes, [7] level-2 boxes walked, [8] level-2 boxes passed,
+ * [9] clusters requested, [10] transposed member tests, [11] their rounds, [12] their far-root
+ * passes, [13] per-lane member tests, [14] sky, [15] hit shading, [16] lambert, [17] unit
+ * direction (metal/dielectric), [18] dielectric, [19] sample stores, [20] metal absorptions.   */
+int rt_scene_debug_events(rt_scene *scene, uint64_t out[32], int reset);
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,
                             void *stream);

@@ -70,6 +70,7 @@ def _declare(L):
         "rt_scene_kernel_times": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_float), P(C.c_uint32)]),
         "rt_scene_debug_counters": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int]),
         "rt_scene_debug_timeline": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
+        "rt_scene_debug_events": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int]),
         "rt_epilogue_rgb8_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     }
     for name, (res, args) in sig.items():

@@ -123,7 +123,10 @@ constexpr uint32_t kQueueStride = 64;
 // V_STATS_LDS diagnostics buffer: 16 counters, then {start, exit, iterations, hw id | refills}
 // per wave
 constexpr uint32_t kDbgWaves = 65536;
-constexpr size_t kDbgWords = 16 + 4 * static_cast<size_t>(kDbgWaves);
+// then kDbgEvents block-execution counters (rt_scene_debug_events)
+constexpr uint32_t kDbgEvents = 32;
+constexpr size_t kDbgEvBase = 16 + 4 * static_cast<size_t>(kDbgWaves);
+constexpr size_t kDbgWords = kDbgEvBase + kDbgEvents;
 
 enum Variant : int { V_EXACT_LDS = 0, V_EXACT_SCALAR = 1, V_FAST_LDS = 2, V_STATS_LDS = 3 };
 

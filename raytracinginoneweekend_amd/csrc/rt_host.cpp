@@ -1211,6 +1211,18 @@ int rt_scene_debug_counters(rt_scene *sc, uint64_t out[16], int reset)
     return RT_OK;
 }
 
+int rt_scene_debug_events(rt_scene *sc, uint64_t out[32], int reset)
+{
+    if (!sc || !out) return fail(RT_ERR_INVALID, "rt_scene_debug_events: null argument");
+    RT_HIP(hipSetDevice(sc->device));
+    std::memset(out, 0, 32 * sizeof(uint64_t));
+    if (!sc->dbg) return RT_OK;
+    RT_HIP(hipDeviceSynchronize());
+    RT_HIP(hipMemcpy(out, sc->dbg + rt::kDbgEvBase, rt::kDbgEvents * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (reset) RT_HIP(hipMemset(sc->dbg + rt::kDbgEvBase, 0, rt::kDbgEvents * sizeof(uint64_t)));
+    return RT_OK;
+}
+
 int rt_scene_debug_timeline(rt_scene *sc, uint64_t *out, uint32_t max_waves, uint32_t *n)
 {
     if (!sc || !out || !n) return fail(RT_ERR_INVALID, "rt_scene_debug_timeline: null argument");

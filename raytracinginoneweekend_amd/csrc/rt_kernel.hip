@@ -53,6 +53,28 @@ __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta)                    
     return (I * eta - adds(N * sqrtf(k), d * eta)) * (k >= 0.f ? 1.f : 0.f);
 }
 
+// Diagnostic counters (STATS builds only; see rt_scene_debug_counters): per-lane tallies
+// plus wave-level ones counted by the first active lane.
+struct Dbg {
+    uint32_t wave_blocks, lane_blocks, wave_roots, lane_roots, wave_member_blocks;
+    uint32_t ev[kDbgEvents];  // executions of the code blocks below by the wave (rt_scene_debug_events)
+};
+__device__ __forceinline__ bool first_active_lane()
+{
+    return (threadIdx.x & 63u) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63u);
+}
+// block-execution events (STATS builds): counted once per wave each time the block runs
+enum DbgEvent : uint32_t {
+    EV_ITER, EV_REFILL_TRIP, EV_FRESH, EV_REJECT_TRIP, EV_LENS_DONE, EV_SCATTER_DONE, EV_ROOT_GATE_PASS,
+    EV_SUPER, EV_SUPER_PASS, EV_CLUSTER_REQ, EV_TRANSPOSED, EV_T_ROUND, EV_T_FAR, EV_PER_LANE_MEMBERS,
+    EV_SKY, EV_HIT, EV_LAMBERT, EV_UNIT_DIR, EV_DIELECTRIC, EV_STORE, EV_METAL_ABSORB, EV_COUNT
+};
+static_assert(EV_COUNT <= kDbgEvents, "event counters");
+#define RT_EV(e)                                          \
+    do {                                                  \
+        if (STATS && first_active_lane()) ++dbg.ev[(e)]; \
+    } while (0)
+
 // ---- RNG: PCG32 XSH-RR per (pixel, sample) stream; the increment is wave-uniform ---------
 __device__ __forceinline__ uint32_t pcg_next(uint64_t &state, uint64_t inc)
 {
@@ -116,7 +138,8 @@ __device__ __forceinline__ f3 random_in_unit_sphere(uint64_t &st, uint64_t inc)
 #ifndef RT_REJECT_CAP
 #define RT_REJECT_CAP 4  // 0: unbounded (the loop runs until every lane accepts)
 #endif
-__device__ __forceinline__ f3 random_in_unit_sphere_capped(uint64_t &st, uint64_t inc, bool &got)
+template <bool STATS>
+__device__ __forceinline__ f3 random_in_unit_sphere_capped(uint64_t &st, uint64_t inc, bool &got, Dbg &dbg)
 {
     if (RT_REJECT_CAP == 0) {
         got = true;
@@ -125,6 +148,7 @@ __device__ __forceinline__ f3 random_in_unit_sphere_capped(uint64_t &st, uint64_
     f3 p = mk(0.f, 0.f, 0.f);
     got = false;
     for (int k = 0; k < (RT_REJECT_CAP > 0 ? RT_REJECT_CAP : 1); ++k) {
+        RT_EV(EV_REJECT_TRIP);
         const float x = canonical_pm1(st, inc);
         const float y = canonical_pm1(st, inc);
         const float z = canonical_pm1(st, inc);
@@ -187,16 +211,6 @@ __device__ __forceinline__ void pixel_of(const FC &fc, uint32_t i, uint32_t &x, 
 // — the same minimum whatever order spheres are visited in, so the scene may be reordered
 // into spatial clusters. Spheres come 8 at a time: 8 discriminants, one
 // max reduction (NaN never wins) and the root work only when some lane needs it.
-// Diagnostic counters (STATS builds only; see rt_scene_debug_counters): per-lane tallies
-// plus wave-level ones counted by the first active lane.
-struct Dbg {
-    uint32_t wave_blocks, lane_blocks, wave_roots, lane_roots, wave_member_blocks;
-};
-__device__ __forceinline__ bool first_active_lane()
-{
-    return (threadIdx.x & 63u) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63u);
-}
-
 struct Hit {  // the closest candidate so far as hit_key(t, original index); ~0 = none
     uint64_t key;
     __device__ float t() const { return __uint_as_float((uint32_t)(key >> 32)); }
@@ -355,10 +369,10 @@ struct TransposeLds {
     float4 ray[kTransposeMax][2];   // {o.x, o.y, o.z, a}, {d.x, d.y, d.z, -}
     uint64_t key[kTransposeMax];
 };
-template <bool FAST>
+template <bool FAST, bool STATS>
 __device__ __forceinline__ void members_transposed(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
                                                    uint32_t start, uint32_t cnt, uint64_t M, bool req,
-                                                   TransposeLds *tw, f3 o, f3 d, float a, Hit &h)
+                                                   TransposeLds *tw, f3 o, f3 d, float a, Hit &h, Dbg &dbg)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m = (uint32_t)__popcll(M);
@@ -375,6 +389,7 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
     const float4 s = geo[start + k];
     const uint32_t sid = sidx[start + k];
     for (uint32_t r0 = 0; r0 < m; r0 += 4u) {
+        RT_EV(EV_T_ROUND);
         const uint32_t r = r0 + (lane >> 4);
         const bool valid = kval && r < m;
         const uint32_t rr = min(r, m - 1u);
@@ -398,6 +413,7 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
             float t = (-b - q) / ra;                                       // :63
             const bool ok = in_range(t);
             if (__ballot(pos && !ok)) {
+                RT_EV(EV_T_FAR);
                 const float t2 = (-b + q) / ra;                            // :76
                 t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
             } else {
@@ -426,12 +442,15 @@ __device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, co
 {
     const uint64_t M = __ballot(req);
     if (!M) return;
+    RT_EV(EV_CLUSTER_REQ);
     const uint32_t scu = __builtin_amdgcn_readfirstlane(scu_lane);
     const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
     wt.sph += (uint64_t)__popcll(M) * cnt;
     if ((uint32_t)__popcll(M) <= tmax && cnt <= 16u) {
-        members_transposed<FAST>(geo, sidx, start, cnt, M, req, tw, o, d, a, h);
+        RT_EV(EV_TRANSPOSED);
+        members_transposed<FAST, STATS>(geo, sidx, start, cnt, M, req, tw, o, d, a, h, dbg);
     } else if (req) {
+        RT_EV(EV_PER_LANE_MEMBERS);
         if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
         run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
     }
@@ -468,12 +487,15 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
             if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)))
                 n_supers = 0;
         }
+        if (n_supers) RT_EV(EV_ROOT_GATE_PASS);
         for (uint32_t g = 0; g < n_supers; ++g) {
+            RT_EV(EV_SUPER);
             const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
             wt.box += lanes(active);
             const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t() * 1.002f);
             const uint64_t spm = __ballot(sp);
             if (!spm) continue;
+            RT_EV(EV_SUPER_PASS);
             const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
             wt.box += 4u * (uint32_t)__popcll(spm);
             for (uint32_t c = c0i; c < c0i + 4; c += 2) {
@@ -554,7 +576,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     // stream state waits in (o.x, o.y) and its jittered (u, v) in (d.x, d.y) until it does
     bool pend_lens = false;
     WaveTally wt{0, 0, 0};
-    Dbg dbg{0, 0, 0, 0, 0};
+    Dbg dbg{};
     uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0;
     uint64_t t_dry = 0;  // STATS: realtime when this wave found every queue empty
     // STATS build only: shader-clock cycles per loop region, summed over the wave's iterations
@@ -598,6 +620,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         bool fresh = false;
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
+            RT_EV(EV_REFILL_TRIP);
             if (cnext >= cend) {
                 uint32_t c = 0;
                 if (lane == 0) c = atomicAdd(p.queue_ctr + q * kQueueStride, 1u);
@@ -663,6 +686,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         uint64_t rc = 0;  // the camera stream of a fresh sample
         float uu = 0.f, vv = 0.f;
         if (fresh) {
+            RT_EV(EV_FRESH);
             uint32_t px, rr;
             pixel_of(*fc, pix, px, rr);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
@@ -701,7 +725,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             }
             uint64_t st = lens ? rc : rng;
             bool got;
-            const f3 r = random_in_unit_sphere_capped(st, inc, got);
+            const f3 r = random_in_unit_sphere_capped<STATS>(st, inc, got, dbg);
             if (!got) {
                 defer = true;
                 if (lens) {
@@ -714,6 +738,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     rng = st;  // pend stays set
                 }
             } else if (lens) {
+                RT_EV(EV_LENS_DONE);
                 pend_lens = false;
                 // camera.hxx:46-57
                 const f3 rd = r * fc->lens;
@@ -724,6 +749,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                      mk(fc->ver[0], fc->ver[1], fc->ver[2]) * (1.f - vv)) - off;
                 if (fc->corrected) d = d - org;
             } else {
+                RT_EV(EV_SCATTER_DONE);
                 rng = st;
                 if (!pend_metal) {
                     d = (d + r) - o;                       // lambert :135, d held p + n, o = p
@@ -733,6 +759,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     if (dot(nd, mk(pn.x, pn.y, pn.z)) > 0.f) {
                         d = nd;
                     } else {                               // absorbed: main.cxx:68, colour 0
+                        RT_EV(EV_METAL_ABSORB);
                         alive = false;
                         float *dst = p.slots + ((size_t)ls * fc->n_pixels + pix) * 3u;
                         dst[0] = 0.f;
@@ -745,6 +772,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         }
         stamp(1);
         if (__ballot(alive) == 0) break;  // only when the item space is exhausted
+        RT_EV(EV_ITER);
         if (STATS && lane == 0) {
             ++dbg_iters;
             if (exhausted) {
@@ -780,6 +808,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                 const uint32_t ib = h.id();
                 ++depth;
                 if (ib == 0xffffffffu) {
+                    RT_EV(EV_SKY);
                     // main.cxx:71: background(.5 * unit_direction.y + 1) * attenuation
                     const float tt = .5f * normalize(d).y + 1.f;
                     const f3 bg = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
@@ -790,6 +819,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     // returns 0 too; this sample's streams are not drawn from again
                     done = true;
                 } else {
+                    RT_EV(EV_HIT);
                     float4 sf, md;
                     uint32_t kind;
                     if (V != V_EXACT_SCALAR && p.shade_lds) {
@@ -810,12 +840,14 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     // raytracer.hxx:120-199
                     o = hp;
                     if (kind == 0u) {                           // lambert, :132-141
+                        RT_EV(EV_LAMBERT);
                         d = hp + hn;                            // + rius next iteration, then - p
                         pend = true;
                         pend_metal = false;
                     } else {
                         // metal and dielectric lanes share one unit direction and one reflection
                         // (one code path for the wave instead of two)
+                        RT_EV(EV_UNIT_DIR);
                         const f3 ud = normalize(d);
                         const f3 rf = reflect(ud, hn);
                         if (kind == 1u) {                       // metal, :143-156
@@ -824,6 +856,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                             pend = true;
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
+                            RT_EV(EV_DIELECTRIC);
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w;
                             float cosv = dot(ud, hn);
@@ -843,6 +876,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             }
             stamp(3);
             if (done) {
+                RT_EV(EV_STORE);
                 // the sample's colour goes to its slot; accumulate_kernel forms the reference's
                 // blocked sum over the slots (main.cxx:205)
                 alive = false;
@@ -871,6 +905,12 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             unsigned long long v = c[i];
             for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
             if (lane == 0) atomicAdd(p.dbg + i, v);
+        }
+#pragma unroll
+        for (int i = 0; i < (int)EV_COUNT; ++i) {
+            unsigned long long v = dbg.ev[i];
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) atomicAdd(p.dbg + kDbgEvBase + i, v);
         }
         if (lane == 0) {
             for (int i = 0; i < 5; ++i) atomicAdd(p.dbg + 8 + i, (unsigned long long)cyc[i]);

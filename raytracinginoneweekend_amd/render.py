@@ -181,6 +181,16 @@ class DeviceScene:
         out["launch_start"] = (~buf[14]) & 0xffffffffffffffff if buf[14] else 0  # 100 MHz ticks
         return out
 
+    EVENTS = ["iter", "refill_trip", "fresh", "reject_trip", "lens_done", "scatter_done", "root_gate_pass", "super",
+              "super_pass", "cluster_req", "transposed", "t_round", "t_far", "per_lane_members", "sky", "hit",
+              "lambert", "unit_dir", "dielectric", "store", "metal_absorb"]
+
+    def debug_events(self, reset=True):
+        """Block-execution counts of the instrumented kernel (RT_DEBUG_STATS=1), see rt_scene_debug_events."""
+        buf = (C.c_uint64 * 32)()
+        check(lib().rt_scene_debug_events(self.handle, buf, 1 if reset else 0))
+        return dict(zip(self.EVENTS, list(buf)))
+
     def debug_timeline(self, max_waves=65536):
         """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry) of the last
         instrumented launch (RT_DEBUG_STATS=1; dry = when the wave found every queue empty; times

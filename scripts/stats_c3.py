@@ -31,10 +31,12 @@ stream = torch.cuda.current_stream().cuda_stream
 ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr())  # warm-up
 torch.cuda.synchronize()
 ds.debug_counters(reset=True)
+ds.debug_events(reset=True)
 seg.zero_()
 ds.render(cam, p, out.data_ptr(), stream, seg.data_ptr())
 torch.cuda.synchronize()
 c = ds.debug_counters(reset=True)
+ev = ds.debug_events(reset=True)
 segments, sph, box = (int(x) for x in seg.cpu())
 n_always = 1 if scene == "huge" else 0
 member_tests = sph - n_always * segments
@@ -49,6 +51,7 @@ res = {
     "blocks_lane_per_wave": c["lane_blocks"] / max(1, c["wave_blocks"]),
     "roots_lane_per_wave": c["lane_roots"] / max(1, c["wave_roots"]),
     "cycle_share": {k: round(c[k] / max(1, cyc), 3) for k in ("cyc_refill", "cyc_start", "cyc_hit", "cyc_shade", "cyc_fold")},
+    "events_per_iter": {k: round(v / max(1, ev["iter"]), 4) for k, v in ev.items()},
     "raw": {k: int(v) for k, v in c.items()},
 }
 print(json.dumps(res, indent=1))

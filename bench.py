@@ -249,8 +249,9 @@ def main():
 
     def measure(cam, steps, warmup):
         """warmup untimed frames, then `steps` frames timed between barriers + syncs (max over
-        ranks), then one frame alone three times (its latency, median); segment counters of
-        the timed frames."""
+        ranks), then one frame alone three times (its latency, median), then one frame of the
+        counting kernel (the same paths and bits, plus tallies of segments and executed tests:
+        the work of every frame of this workload, which the timed frames do not tally)."""
         def step(count_segments):
             ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
             if rgb8:
@@ -268,10 +269,9 @@ def main():
         if distributed:
             dist.barrier()
         torch.cuda.synchronize()
-        seg.zero_()
         t0 = time.perf_counter()
         for _ in range(steps):
-            step(True)
+            step(False)
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
@@ -288,7 +288,11 @@ def main():
             torch.cuda.synchronize()
             lat.append(time.perf_counter() - t1)
         latency = sorted(lat)[1]
-        counts = [int(x) for x in seg.tolist()]
+        torch.cuda.synchronize()
+        seg.zero_()
+        step(True)
+        torch.cuda.synchronize()
+        counts = [int(x) * steps for x in seg.tolist()]  # per frame x timed frames
         counts_all = counts
         if distributed:
             t = torch.tensor([elapsed, latency], dtype=torch.float64, device=dev)
@@ -388,7 +392,7 @@ def main():
         }
         v = {"exact": 0, "scalar": 1, "fast": 2}[args.variant]
         cull = 0 if args.traversal == "brute" or v == 1 else 7
-        kname = f"render_kernel<{v}, {cull}, false>"
+        kname = f"render_kernel<{v}, {cull}, false, false>"
         pmc, status = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
                                                    "traversal": args.traversal, "n_gpus": world})
         rec["roofline"]["pmc_status"] = status

@@ -74,6 +74,8 @@ def _declare(L):
         "rt_epilogue_rgb8_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("RT_LIB_PATH") and not hasattr(L, name):
+            continue  # an older build under A/B may lack newer entry points
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

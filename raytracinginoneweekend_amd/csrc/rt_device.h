@@ -71,6 +71,7 @@ struct KParams {
     uint32_t n_supers, supers_offset;  // level 2: groups of 4 consecutive clusters, 2 float4 each
     uint32_t use_root;       // level 3: one box over all clusters at supers_offset + 2 n_supers
     uint32_t transpose_max;  // clusters requested by at most this many lanes (<= 16) are tested transposed
+    uint32_t fast_roots;     // scene and camera within 2^19 of the origin: short exact root forms (rt_kernel.hip RayDiv)
     float clus_pad;          // max over clusters of 1e-3 * (|C|_1 + |e|_1) + 1e-6 (per-ray pad adds 1e-3 |o|_1)
     // shading records in the blob at shade_offset, indexed by original sphere index:
     // {cx, cy, cz, r}, {albedo rgb, param} x n_spheres, then n_spheres kind bytes (16-B padded)

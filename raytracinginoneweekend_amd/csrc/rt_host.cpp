@@ -170,6 +170,7 @@ struct rt_scene {
     float clus_pad[2] = {0.f, 0.f};
     uint32_t n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     uint32_t shade_offset[2] = {0, 0};
+    bool in_fast_range = false;  // every sphere within 2^19 of the origin (short exact root forms)
     // workspaces: consecutive render passes (of one frame or of consecutive frames) rotate over
     // internal streams xs[b] and workspaces slots[b], so a pass renders while the caller stream
     // still accumulates the previous ones
@@ -651,6 +652,21 @@ uint32_t transpose_max_env()
     return static_cast<uint32_t>(std::min<unsigned long>(v, 16ul));
 }
 
+// Short exact root forms (rt_kernel.hip RayDiv) when the scene and the camera lie within 2^19 of
+// the origin; RT_FAST_ROOTS=0 keeps the IEEE sqrt/division sequences (A/B, tests); same bits.
+bool fast_roots_env()
+{
+    const char *e = std::getenv("RT_FAST_ROOTS");
+    return !(e && e[0] == '0');
+}
+bool camera_in_fast_range(const rt_camera &c)
+{
+    for (int i = 0; i < 3; ++i)
+        for (float v : {c.origin[i], c.lower_left_corner[i], c.horizontal[i], c.vertical[i]})
+            if (!(std::fabs(v) <= 0x1p19f)) return false;
+    return std::fabs(c.lens_radius) <= 0x1p19f;
+}
+
 // RT_ROOT_BOX=0 disables the level-3 box gate (A/B); same bits either way.
 uint32_t root_box_env()
 {
@@ -833,6 +849,10 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     }
     rt_scene *sc = new rt_scene();
     for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
+    sc->in_fast_range = true;
+    for (uint32_t i = 0; i < n_spheres; ++i)
+        for (float v : {spheres[i].center[0], spheres[i].center[1], spheres[i].center[2], spheres[i].radius})
+            if (!(std::fabs(v) <= 0x1p19f)) sc->in_fast_range = false;
     sc->device = device;
     sc->n_spheres = n_spheres;
     sc->n_materials = n_materials;
@@ -994,6 +1014,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     k.supers_offset = sc->supers_offset[b];
     k.use_root = root_box_env();
     k.transpose_max = transpose_max_env();
+    k.fast_roots = sc->in_fast_range && camera_in_fast_range(*camera) && fast_roots_env() ? 1u : 0u;
     k.shade_offset = sc->shade_offset[b];
     // the shading records (the blob's tail) join the geometry in LDS unless that costs
     // workgroups per CU; RT_SHADE_LDS=0/1 forces the choice for A/B

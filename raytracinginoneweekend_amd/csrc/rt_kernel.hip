@@ -221,8 +221,13 @@ constexpr uint64_t kNoHit = 0x7f7fffffffffffffull;  // t = kMAX, index = none
 // Work counters of one wave (wave-uniform, scalar registers): segments traced and the
 // lane-level ray-sphere and cluster-box tests executed, summed from ballots in uniform control
 // flow (a test the wave runs for k requesting lanes counts k).
+// Only the counting instantiation (COUNT, used when the caller asks for the counters) keeps them.
+template <bool COUNT>
 struct WaveTally {
-    uint64_t seg, sph, box;
+    uint64_t seg = 0, sph = 0, box = 0;
+    __device__ __forceinline__ void add_seg(uint32_t n) { if (COUNT) seg += n; }
+    __device__ __forceinline__ void add_sph(uint64_t n) { if (COUNT) sph += n; }
+    __device__ __forceinline__ void add_box(uint32_t n) { if (COUNT) box += n; }
 };
 __device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(__ballot(x)); }
 
@@ -242,10 +247,68 @@ __device__ __forceinline__ uint64_t hit_key(float t, uint32_t id)
     return ((uint64_t)__float_as_uint(t) << 32) | id;
 }
 
+// ---- the root of a candidate (raytracer.hxx:62-90) -----------------------------------------
+// The IEEE forms of sqrtf and of division, as the compiler expands them, scale operands whose
+// exponents are extreme and fix up special values; when neither can occur they reduce to shorter
+// exact sequences. Per ray segment the divisor a = |d|^2 gets its refined reciprocal once (the
+// divisor-only head of the division sequence). fd (wave-uniform) says the short forms give the
+// IEEE bits for every lane: the scene lies within 2^19 of the origin (KParams::fast_roots: then
+// |oc| <= 2^21 and every in-range root is below 2^43) and every active lane has a in
+// [2^-40, 2^40], so no root division needs scaling (quotient exponents stay 96 below the
+// numerator's) and every discriminant is below 2^96.
+struct RayDiv {
+    float a, y;  // divisor |d|^2 and its refined reciprocal
+    bool fd;     // wave-uniform: the short forms are exact for every lane
+};
+__device__ __forceinline__ RayDiv ray_div(float a, bool active, uint32_t fast_roots)
+{
+    const float y0 = __builtin_amdgcn_rcpf(a);
+    const float y = fmaf(fmaf(-a, y0, 1.f), y0, y0);
+    const bool ok = a >= 0x1p-40f && a <= 0x1p40f;
+    return {a, y, fast_roots != 0u && !__ballot(active && !ok)};
+}
+// n / a: the IEEE sequence (v_div_scale, rcp + refinement, two FMA corrections, v_div_fmas,
+// v_div_fixup) with no scaling and no special value, i.e. its two corrections
+__device__ __forceinline__ float div_ray(float n, const RayDiv &r)
+{
+    const float q0 = n * r.y;
+    const float q1 = fmaf(fmaf(-r.a, q0, n), r.y, q0);
+    return fmaf(fmaf(-r.a, q1, n), r.y, q1);
+}
+// correctly rounded sqrt for 0 < x < 2^96: the compiler's IEEE expansion (v_sqrt_f32, then the
+// one-ulp neighbours checked by FMA residuals) always run on x * 2^32 and scaled back by 2^-16,
+// both exact, so the result is that of the expansion's own small-input path for every such x
+__device__ __forceinline__ float sqrt_scaled(float x)
+{
+    const float xs = x * 0x1p32f;
+    const float s = __builtin_amdgcn_sqrtf(xs);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sup = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = fmaf(-sdn, s, xs) <= 0.f ? sdn : s;
+    r = fmaf(-sup, s, xs) > 0.f ? sup : r;
+    return r * 0x1p-16f;
+}
+// the near root (-b - sqrt(disc)) / a and its sqrt, raytracer.hxx:62-63
+__device__ __forceinline__ float near_root(float b, float disc, const RayDiv &r, float &q)
+{
+    if (r.fd) {
+        q = sqrt_scaled(disc);
+        return div_ray(-b - q, r);
+    }
+    q = sqrtf(disc);
+    return (-b - q) / r.a;
+}
+// the far root (-b + sqrt(disc)) / a, raytracer.hxx:76
+__device__ __forceinline__ float far_root(float b, float q, const RayDiv &r)
+{
+    return r.fd ? div_ray(-b + q, r) : (-b + q) / r.a;
+}
+
 template <bool FAST, bool STATS, int N = 8>
 __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx, uint32_t i,
-                                            f3 o, f3 d, float a, Hit &h, Dbg &dbg)
+                                            f3 o, f3 d, const RayDiv &rd, Hit &h, Dbg &dbg)
 {
+    const float a = rd.a;
     float bq[N], dq[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
@@ -282,11 +345,11 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
             const bool pos = dq[k] > 0.f;                                    // :62
             if (__ballot(pos)) {
                 if (STATS) { dbg.lane_roots += pos; if (first_active_lane()) ++dbg.wave_roots; }
-                const float q = sqrtf(dq[k]);
-                float t = (-bq[k] - q) / a;                                  // :63
+                float q;
+                float t = near_root(bq[k], dq[k], rd, q);                    // :63
                 const bool ok = in_range(t);
                 if (__ballot(pos && !ok)) {
-                    const float t2 = (-bq[k] + q) / a;                       // :76
+                    const float t2 = far_root(bq[k], q, rd);                 // :76
                     t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
                 } else {
                     t = ok ? t : __builtin_nanf("");
@@ -308,13 +371,14 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
 // multiples of 4; the always-tested list has its exact count, e.g. 1 for the ground)
 template <bool FAST, bool STATS>
 __device__ __forceinline__ void run_members(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
-                                            uint32_t start, uint32_t cnt, f3 o, f3 d, float a, Hit &h, Dbg &dbg)
+                                            uint32_t start, uint32_t cnt, f3 o, f3 d, const RayDiv &rd, Hit &h,
+                                            Dbg &dbg)
 {
     const uint32_t end = start + cnt;
     uint32_t i = start;
-    for (; i + 8 <= end; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, a, h, dbg);
-    if (i + 4 <= end) { test_block8<FAST, STATS, 4>(geo, sidx, i, o, d, a, h, dbg); i += 4; }
-    for (; i < end; ++i) test_block8<FAST, STATS, 1>(geo, sidx, i, o, d, a, h, dbg);
+    for (; i + 8 <= end; i += 8) test_block8<FAST, STATS>(geo, sidx, i, o, d, rd, h, dbg);
+    if (i + 4 <= end) { test_block8<FAST, STATS, 4>(geo, sidx, i, o, d, rd, h, dbg); i += 4; }
+    for (; i < end; ++i) test_block8<FAST, STATS, 1>(geo, sidx, i, o, d, rd, h, dbg);
 }
 
 struct RayBox {  // per-segment constants of the padded slab test
@@ -366,20 +430,21 @@ __device__ __forceinline__ uint64_t min16_key(uint64_t k)
 }
 // per-wave LDS of the transposed tests: the requesting rays by rank, and each ray's minimum
 struct TransposeLds {
-    float4 ray[kTransposeMax][2];   // {o.x, o.y, o.z, a}, {d.x, d.y, d.z, -}
+    float4 ray[kTransposeMax][2];   // {o.x, o.y, o.z, a}, {d.x, d.y, d.z, refined 1/a}
     uint64_t key[kTransposeMax];
 };
 template <bool FAST, bool STATS>
 __device__ __forceinline__ void members_transposed(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
                                                    uint32_t start, uint32_t cnt, uint64_t M, bool req,
-                                                   TransposeLds *tw, f3 o, f3 d, float a, Hit &h, Dbg &dbg)
+                                                   TransposeLds *tw, f3 o, f3 d, const RayDiv &rd, Hit &h,
+                                                   Dbg &dbg)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t m = (uint32_t)__popcll(M);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
     if (req) {
-        tw->ray[rank][0] = make_float4(o.x, o.y, o.z, a);
-        tw->ray[rank][1] = make_float4(d.x, d.y, d.z, 0.f);
+        tw->ray[rank][0] = make_float4(o.x, o.y, o.z, rd.a);
+        tw->ray[rank][1] = make_float4(d.x, d.y, d.z, rd.y);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -395,6 +460,7 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
         const uint32_t rr = min(r, m - 1u);
         const float4 q0 = tw->ray[rr][0], q1 = tw->ray[rr][1];
         const float ra = q0.w;                                              // |d|^2, as closest_hit
+        const RayDiv rdr{ra, q1.w, rd.fd};
         const float ocx = q0.x - s.x, ocy = q0.y - s.y, ocz = q0.z - s.z;  // raytracer.hxx:55
         float b, disc;
         if (FAST) {
@@ -409,12 +475,12 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
         const bool pos = valid && disc > 0.f;                              // :62
         uint64_t key = ~0ull;
         if (__ballot(pos)) {
-            const float q = sqrtf(disc);
-            float t = (-b - q) / ra;                                       // :63
+            float q;
+            float t = near_root(b, disc, rdr, q);                          // :63
             const bool ok = in_range(t);
             if (__ballot(pos && !ok)) {
                 RT_EV(EV_T_FAR);
-                const float t2 = (-b + q) / ra;                            // :76
+                const float t2 = far_root(b, q, rdr);                      // :76
                 t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
             } else {
                 t = ok ? t : __builtin_nanf("");
@@ -435,35 +501,36 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-template <bool FAST, bool STATS>
+template <bool FAST, bool STATS, bool COUNT>
 __device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, const float4 *__restrict__ geo,
                                                  const uint32_t *__restrict__ sidx, TransposeLds *tw, uint32_t tmax,
-                                                 f3 o, f3 d, float a, Hit &h, Dbg &dbg, WaveTally &wt)
+                                                 f3 o, f3 d, const RayDiv &rd, Hit &h, Dbg &dbg, WaveTally<COUNT> &wt)
 {
     const uint64_t M = __ballot(req);
     if (!M) return;
     RT_EV(EV_CLUSTER_REQ);
     const uint32_t scu = __builtin_amdgcn_readfirstlane(scu_lane);
     const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
-    wt.sph += (uint64_t)__popcll(M) * cnt;
+    wt.add_sph((uint64_t)__popcll(M) * cnt);
     if ((uint32_t)__popcll(M) <= tmax && cnt <= 16u) {
         RT_EV(EV_TRANSPOSED);
-        members_transposed<FAST, STATS>(geo, sidx, start, cnt, M, req, tw, o, d, a, h, dbg);
+        members_transposed<FAST, STATS>(geo, sidx, start, cnt, M, req, tw, o, d, rd, h, dbg);
     } else if (req) {
         RT_EV(EV_PER_LANE_MEMBERS);
         if (STATS && first_active_lane()) dbg.wave_member_blocks += (cnt + 7) / 8;
-        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, a, h, dbg);
+        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, rd, h, dbg);
     }
 }
 
-template <bool FAST, int CULL, bool STATS>
+template <bool FAST, int CULL, bool STATS, bool COUNT>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
-                                           f3 d, Dbg &dbg, WaveTally &wt, bool active, TransposeLds *tw)
+                                           f3 d, Dbg &dbg, WaveTally<COUNT> &wt, bool active, TransposeLds *tw)
 {
     const float a = d.x * d.x + d.y * d.y + d.z * d.z;
+    const RayDiv rd = ray_div(a, active, p.fast_roots);
     Hit h{kNoHit};
-    run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, a, h, dbg);
+    run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
     if (CULL) {
         auto safe_rcp = [](float x) {
             return __builtin_amdgcn_rcpf(fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x);
@@ -483,7 +550,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         const float4 *sup = clus + (p.supers_offset - p.clus_offset);
         uint32_t n_supers = p.n_supers;
         if (p.use_root) {
-            wt.box += lanes(active);
+            wt.add_box(lanes(active));
             if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)))
                 n_supers = 0;
         }
@@ -491,20 +558,20 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         for (uint32_t g = 0; g < n_supers; ++g) {
             RT_EV(EV_SUPER);
             const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
-            wt.box += lanes(active);
+            wt.add_box(lanes(active));
             const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t() * 1.002f);
             const uint64_t spm = __ballot(sp);
             if (!spm) continue;
             RT_EV(EV_SUPER_PASS);
             const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
-            wt.box += 4u * (uint32_t)__popcll(spm);
+            wt.add_box(4u * (uint32_t)__popcll(spm));
             for (uint32_t c = c0i; c < c0i + 4; c += 2) {
                 const float tb_now = h.t() * 1.002f;
                 const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
                 const bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
-                cluster_members7<FAST, STATS>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
+                cluster_members7<FAST, STATS, COUNT>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, rd, h,
                                               dbg, wt);
-                cluster_members7<FAST, STATS>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, a, h,
+                cluster_members7<FAST, STATS, COUNT>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, rd, h,
                                               dbg, wt);
             }
         }
@@ -521,7 +588,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
 // path reloads (measured: 5.03-5.06 ms vs 5.19-5.24 per config-3 launch).
 template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? 6 : RT_MIN_WAVES_PER_SIMD;
-template <int V, int CULL, bool STATS>
+template <int V, int CULL, bool STATS, bool COUNT>
 __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kernel(const KParams p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
@@ -575,7 +642,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     // a fresh sample whose lens draw did not finish within RT_REJECT_CAP attempts: its camera
     // stream state waits in (o.x, o.y) and its jittered (u, v) in (d.x, d.y) until it does
     bool pend_lens = false;
-    WaveTally wt{0, 0, 0};
+    WaveTally<COUNT> wt;
     Dbg dbg{};
     uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0;
     uint64_t t_dry = 0;  // STATS: realtime when this wave found every queue empty
@@ -785,16 +852,16 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         const bool seg = alive && !defer && depth < p.max_depth;  // depth check: main.cxx:74
         Hit h{kNoHit};
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
-            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, wt, seg, tw);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, dbg, wt, seg, tw);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
-            h = closest_hit<FAST, CULL, STATS>(p, geo, sidx, clus, o, d, dbg, wt, true, nullptr);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, dbg, wt, true, nullptr);
         }
         stamp(2);
         {
             const uint32_t ns = lanes(seg);  // segments of this iteration (main.cxx:74 passed)
-            wt.seg += ns;
-            wt.sph += (uint64_t)ns * p.n_always;
+            wt.add_seg(ns);
+            wt.add_sph((uint64_t)ns * p.n_always);
         }
 
         // ---- shading: the hit of every live lane -----------------------------------------
@@ -888,7 +955,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         }
     }
 
-    if (p.segments) {
+    if (COUNT && p.segments) {
         // wave reductions, one atomic per wave and counter: [0] segments, [1] sphere tests,
         // [2] cluster box tests (lane-level, executed)
         if (lane == 0) {  // one atomic per wave and counter
@@ -1180,26 +1247,32 @@ __global__ __launch_bounds__(256) void epilogue_rgb8_kernel(const float *in, uin
 // ---- launchers (called from rt_host.cpp) ---------------------------------------------
 // cull: 0 = brute force (every sphere, index order), 7 = two-level cluster walk with
 // transposed member tests (the default)
-template <int V, bool STATS> static const void *ptr_cull(int cull)
+// COUNT: the instantiation that tallies segments and tests (when the caller passes counters)
+template <int V, bool STATS, bool COUNT> static const void *ptr_cull(int cull)
 {
-    if (cull == 7) return reinterpret_cast<const void *>(&render_kernel<V, 7, STATS>);
-    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS>);
+    if (cull == 7) return reinterpret_cast<const void *>(&render_kernel<V, 7, STATS, COUNT>);
+    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, COUNT>);
 }
 
-static const void *render_ptr(int variant, int cull)
+template <bool COUNT> static const void *render_ptr_c(int variant, int cull)
 {
     switch (variant) {
-    case V_EXACT_LDS: return ptr_cull<V_EXACT_LDS, false>(cull);
-    case V_FAST_LDS: return ptr_cull<V_FAST_LDS, false>(cull);
-    case V_EXACT_SCALAR: return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false>);
-    case V_STATS_LDS: return ptr_cull<V_EXACT_LDS, true>(cull);
+    case V_EXACT_LDS: return ptr_cull<V_EXACT_LDS, false, COUNT>(cull);
+    case V_FAST_LDS: return ptr_cull<V_FAST_LDS, false, COUNT>(cull);
+    case V_EXACT_SCALAR:
+        return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false, COUNT>);
+    case V_STATS_LDS: return ptr_cull<V_EXACT_LDS, true, true>(cull);
     default: return nullptr;
     }
+}
+static const void *render_ptr(int variant, int cull, bool count)
+{
+    return count ? render_ptr_c<true>(variant, cull) : render_ptr_c<false>(variant, cull);
 }
 
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream)
 {
-    const void *fn = render_ptr(variant, cull);
+    const void *fn = render_ptr(variant, cull, p.segments != nullptr);
     if (!fn) return hipErrorInvalidValue;
     const size_t lds = (size_t)p.lds_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};
@@ -1208,7 +1281,7 @@ hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid,
 
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds)
 {
-    const void *fn = render_ptr(variant, cull);
+    const void *fn = render_ptr(variant, cull, false);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
 }

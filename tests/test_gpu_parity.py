@@ -19,8 +19,10 @@ pytestmark = pytest.mark.gpu
 RENDERS = sorted(n for n, m in G.manifest()["renders"].items() if m["rng"] == "pcg")
 # clustered0: the same two-level walk with every cluster's members tested per lane (never
 # transposed, RT_TRANSPOSE_MAX=0)
+# ieee_roots: the IEEE sqrt/division sequences for the roots instead of their short exact forms
+# (RT_FAST_ROOTS=0; rt_kernel.hip RayDiv)
 VARIANTS = {"clustered": {}, "clustered0": {"_transpose": "0"}, "brute": {"brute_force": True},
-            "scalar": {"scalar_scene": True}}
+            "scalar": {"scalar_scene": True}, "ieee_roots": {"_env": ("RT_FAST_ROOTS", "0")}}
 
 
 def _params(meta, **kw):
@@ -53,6 +55,8 @@ def test_golden_render_f32(name, variant, monkeypatch):
     kw = dict(VARIANTS[variant])
     if "_transpose" in kw:
         monkeypatch.setenv("RT_TRANSPOSE_MAX", kw.pop("_transpose"))
+    if "_env" in kw:
+        monkeypatch.setenv(*kw.pop("_env"))
     img, st = rt.render_f32(scene, _params(meta, **kw), cam)
     _bits_equal(img, f32)
     assert st.primaries == meta["width"] * meta["num_rows"] * meta["spp"]
@@ -164,6 +168,11 @@ def test_device_api_matches_host_api():
     torch.cuda.synchronize()
     _bits_equal(out.cpu().numpy(), host)
     assert int(seg[0].item()) > 128 * 72 * 4
+    # without counters the non-counting instantiation renders: the same bits
+    out.zero_()
+    ds.render(cam, p, out.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    _bits_equal(out.cpu().numpy(), host)
     u8 = torch.empty((72, 128, 3), dtype=torch.uint8, device="cuda:0")
     rt.epilogue_rgb8_device(out.data_ptr(), u8.data_ptr(), 128 * 72, stream.cuda_stream)
     torch.cuda.synchronize()
@@ -197,6 +206,8 @@ def _random_scene(rng, n, spread, center=(0.0, 0.0, 0.0)):
     (2, 1500, 30.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_REFERENCE),
     (3, 400, 3.0, (0.0, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
     (4, 800, 5.0, (200.0, 0.0, -150.0), abi.RT_CAMERA_CORRECTED),
+    # a scene beyond 2^19 of the origin: the kernel keeps the IEEE root sequences
+    (5, 300, 4.0, (7.0e5, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
 ])
 @pytest.mark.parametrize("transpose", ["0", "4", "16"])
 def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, transpose, monkeypatch):

@@ -846,6 +846,20 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         const size_t at = b.data.size();
         b.data.resize(at + kinds.size() / 4);
         std::memcpy(b.data.data() + at, kinds.data(), kinds.size());
+        // dielectric constants per sphere index (raytracer.hxx:166-174 and the Schlick ratio
+        // :47): {1 / ior, (1 - ior) / (1 + ior), (1 - 1/ior) / (1 + 1/ior), 0}, the same
+        // binary32 operations the kernel would run (this file is built with -ffp-contract=off)
+        for (uint32_t i = 0; i < n_spheres; ++i) {
+            const rt_material &mt = materials[spheres[i].material];
+            float dc[4] = {0.f, 0.f, 0.f, 0.f};
+            if (mt.kind == RT_DIELECTRIC) {
+                const float ior = mt.param, inv = 1.f / ior;
+                dc[0] = inv;
+                dc[1] = (1.f - ior) / (1.f + ior);
+                dc[2] = (1.f - inv) / (1.f + inv);
+            }
+            b.data.insert(b.data.end(), dc, dc + 4);
+        }
     }
     rt_scene *sc = new rt_scene();
     for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;

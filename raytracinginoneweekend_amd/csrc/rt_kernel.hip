@@ -46,11 +46,12 @@ __device__ __forceinline__ f3 normalize(f3 a)                    // math.hxx:219
     return fabsf(l) > FLT_MIN ? a / l : a;
 }
 __device__ __forceinline__ f3 reflect(f3 I, f3 N) { return I - (N * dot(N, I)) * 2.f; } // math.hxx:294-298
+__device__ __forceinline__ float sqrt_scaled(float x);
 __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta)                          // math.hxx:300-309
 {
     const float d = dot(N, I);
     const float k = 1.f - eta * eta * (1.f - d * d);
-    return (I * eta - adds(N * sqrtf(k), d * eta)) * (k >= 0.f ? 1.f : 0.f);
+    return (I * eta - adds(N * sqrt_scaled(k), d * eta)) * (k >= 0.f ? 1.f : 0.f);  // k <= 1
 }
 
 // Diagnostic counters (STATS builds only; see rt_scene_debug_counters): per-lane tallies
@@ -164,9 +165,10 @@ __device__ __forceinline__ f3 random_in_unit_sphere_capped(uint64_t &st, uint64_
 // raytracer.hxx:45-50. std::pow(float,int) promotes to double: r0 = x^2 is exact in double;
 // (1-cos)^5 is formed as y^4 * y with y^4 = y^2*y^2 split exactly by an FMA, so the double
 // product is within a few 1e-17 relative of glibc's pow before the final cast to float.
-__device__ __forceinline__ float schlick(float ri, float c)
+// xf = (1 - ri) / (1 + ri) in binary32 (per sphere and side, from the host).
+__device__ __forceinline__ float schlick_x(float xf, float c)
 {
-    double x = (double)((1.f - ri) / (1.f + ri));
+    double x = (double)xf;
     double r0 = x * x;
     double y = (double)(1.f - c);
     double y2 = y * y;                  // exact (24-bit * 24-bit)
@@ -175,6 +177,7 @@ __device__ __forceinline__ float schlick(float ri, float c)
     double y5 = fma(y4, y, y4lo * y);
     return (float)(r0 + (1.0 - r0) * y5);
 }
+__device__ __forceinline__ float schlick(float ri, float c) { return schlick_x((1.f - ri) / (1.f + ri), c); }
 
 // ---- work decomposition ----------------------------------------------------------------
 __device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t m, uint32_t l)
@@ -525,10 +528,9 @@ __device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, co
 template <bool FAST, int CULL, bool STATS, bool COUNT>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
-                                           f3 d, Dbg &dbg, WaveTally<COUNT> &wt, bool active, TransposeLds *tw)
+                                           f3 d, const RayDiv &rd, Dbg &dbg, WaveTally<COUNT> &wt, bool active,
+                                           TransposeLds *tw)
 {
-    const float a = d.x * d.x + d.y * d.y + d.z * d.z;
-    const RayDiv rd = ray_div(a, active, p.fast_roots);
     Hit h{kNoHit};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
     if (CULL) {
@@ -850,12 +852,16 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
 
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && !defer && depth < p.max_depth;  // depth check: main.cxx:74
+        // |d|^2 (raytracer.hxx:56) and its refined reciprocal for this segment's roots; the sky
+        // below reuses both (unit_direction's length is sqrt of the same sum)
+        const float a = d.x * d.x + d.y * d.y + d.z * d.z;
+        const RayDiv rd = ray_div(a, seg, p.fast_roots);
         Hit h{kNoHit};
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
-            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, dbg, wt, seg, tw);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, seg, tw);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
-            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, dbg, wt, true, nullptr);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, true, nullptr);
         }
         stamp(2);
         {
@@ -876,8 +882,19 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                 ++depth;
                 if (ib == 0xffffffffu) {
                     RT_EV(EV_SKY);
-                    // main.cxx:71: background(.5 * unit_direction.y + 1) * attenuation
-                    const float tt = .5f * normalize(d).y + 1.f;
+                    // main.cxx:71: background(.5 * unit_direction.y + 1) * attenuation. With the
+                    // short forms (rd.fd: a in [2^-40, 2^40]) the length is sqrt_scaled(a) >= 2^-20
+                    // and d.y / length is exact unless |d.y| < 2^-100, where both forms give
+                    // |y| < 2^-80 and tt rounds to 1 either way.
+                    float uy;
+                    if (rd.fd) {
+                        const float l = sqrt_scaled(a);
+                        const float y0 = __builtin_amdgcn_rcpf(l);
+                        uy = div_ray(d.y, RayDiv{l, fmaf(fmaf(-l, y0, 1.f), y0, y0), true});
+                    } else {
+                        uy = normalize(d).y;
+                    }
+                    const float tt = .5f * uy + 1.f;
                     const f3 bg = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
                     col = bg * att;
                     done = true;
@@ -924,18 +941,22 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
                             RT_EV(EV_DIELECTRIC);
+                            // {1 / ior, x(ior), x(1 / ior)} of this sphere, x(r) = (1 - r) / (1 + r)
+                            const float4 dcs = (V != V_EXACT_SCALAR && p.shade_lds ? blob : p.blob)
+                                [p.shade_offset + 2 * p.n_spheres + (p.n_spheres + 15u) / 16u + ib];
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
-                            float ri = md.w;
+                            float ri = md.w, xs = dcs.y;
                             float cosv = dot(ud, hn);
                             if (cosv <= 0.f) {
                                 outward = outward * -1.f;
-                                ri = 1.f / ri;
+                                ri = dcs.x;                     // 1.f / ri
+                                xs = dcs.z;
                                 cosv *= -1.f;
                             }
                             const f3 refr = refract(ud, outward, ri);
                             float prob = 1.f;
                             // length(refr) > 0 <=> norm > 0 (correctly rounded sqrt; NaN -> false)
-                            if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick(ri, cosv);
+                            if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick_x(xs, cosv);
                             d = canonical(rng, inc_data) < prob ? rf : refr;
                         }
                     }

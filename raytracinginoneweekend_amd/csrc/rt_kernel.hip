@@ -77,19 +77,24 @@ static_assert(EV_COUNT <= kDbgEvents, "event counters");
     } while (0)
 
 // ---- RNG: PCG32 XSH-RR per (pixel, sample) stream; the increment is wave-uniform ---------
-__device__ __forceinline__ uint32_t pcg_next(uint64_t &state, uint64_t inc)
+constexpr uint64_t kPcgMul = 6364136223846793005ULL;
+__device__ __forceinline__ uint32_t pcg_out(uint64_t old)
 {
-    uint64_t old = state;
-    state = old * 6364136223846793005ULL + inc;
     uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
     uint32_t rot = (uint32_t)(old >> 59u);
     return (xs >> rot) | (xs << ((0u - rot) & 31u));
+}
+__device__ __forceinline__ uint32_t pcg_next(uint64_t &state, uint64_t inc)
+{
+    uint64_t old = state;
+    state = old * kPcgMul + inc;
+    return pcg_out(old);
 }
 __device__ __forceinline__ uint64_t pcg_seed(uint64_t initstate, uint64_t inc)
 {
     uint64_t st = inc;  // state = 0; next() -> 0 * M + inc
     st += initstate;
-    return st * 6364136223846793005ULL + inc;
+    return st * kPcgMul + inc;
 }
 // libstdc++ generate_canonical<float,24> over a 32-bit engine: float(x) / 2^32, kept < 1.
 // float(x) rounds up to 2^32 for the top 128 words; clamping it to the largest float below,
@@ -146,15 +151,30 @@ __device__ __forceinline__ f3 random_in_unit_sphere_capped(uint64_t &st, uint64_
         got = true;
         return random_in_unit_sphere(st, inc);
     }
-    f3 p = mk(0.f, 0.f, 0.f);
+    // p is written on every attempt a lane makes: a lane that accepted has left the loop, so
+    // later attempts do not touch its p, and no per-attempt select is needed (p of a lane that
+    // did not accept is not used)
+    // The LCG multiplier's halves and the 2^-31 scale sit in VGPRs for the loop (three moves
+    // of literals): on gfx950 a VALU operation reading an SGPR issues at half rate
+    // (scripts/ubench_int.hip), and the compiler would keep these uniform constants in SGPRs.
+    uint32_t m_lo = (uint32_t)kPcgMul, m_hi = (uint32_t)(kPcgMul >> 32);
+    float k31 = 0x1p-31f;
+    asm volatile("" : "+v"(m_lo), "+v"(m_hi), "+v"(k31));
+    const uint64_t mul = ((uint64_t)m_hi << 32) | m_lo;
+    auto draw = [&]() {
+        const uint64_t old = st;
+        st = old * mul + inc;
+        return fmaf(fminf((float)pcg_out(old), 0x1.fffffep31f), k31, -1.f);  // canonical_pm1
+    };
+    f3 p;
     got = false;
+#pragma unroll
     for (int k = 0; k < (RT_REJECT_CAP > 0 ? RT_REJECT_CAP : 1); ++k) {
         RT_EV(EV_REJECT_TRIP);
-        const float x = canonical_pm1(st, inc);
-        const float y = canonical_pm1(st, inc);
-        const float z = canonical_pm1(st, inc);
-        if (!(x * x + y * y + z * z > 0x1.000002p+0f)) {
-            p = mk(x, y, z);
+        p.x = draw();
+        p.y = draw();
+        p.z = draw();
+        if (!(p.x * p.x + p.y * p.y + p.z * p.z > 0x1.000002p+0f)) {
             got = true;
             break;
         }
@@ -232,7 +252,11 @@ struct WaveTally {
     __device__ __forceinline__ void add_sph(uint64_t n) { if (COUNT) sph += n; }
     __device__ __forceinline__ void add_box(uint32_t n) { if (COUNT) box += n; }
 };
-__device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(__ballot(x)); }
+// The lane mask of a predicate, straight from the compare that forms it. (HIP's __ballot takes
+// an int, so the predicate is first materialised as 0/1 in a VGPR and compared again: two extra
+// half-rate VALU operations per vote.)
+__device__ __forceinline__ uint64_t ballot(bool x) { return __builtin_amdgcn_ballot_w64(x); }
+__device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(ballot(x)); }
 
 // t in (kMIN, kMAX), the reference's test (raytracer.hxx:63-64,76-77): positive binary32 values
 // are ordered as their bit patterns, and as unsigned integers every negative value and every
@@ -268,7 +292,7 @@ __device__ __forceinline__ RayDiv ray_div(float a, bool active, uint32_t fast_ro
     const float y0 = __builtin_amdgcn_rcpf(a);
     const float y = fmaf(fmaf(-a, y0, 1.f), y0, y0);
     const bool ok = a >= 0x1p-40f && a <= 0x1p40f;
-    return {a, y, fast_roots != 0u && !__ballot(active && !ok)};
+    return {a, y, fast_roots != 0u && !ballot(active && !ok)};
 }
 // n / a: the IEEE sequence (v_div_scale, rcp + refinement, two FMA corrections, v_div_fmas,
 // v_div_fixup) with no scaling and no special value, i.e. its two corrections
@@ -341,17 +365,17 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
     // lane costs the same issue slots as a computing one, and uniform branches need no
     // exec-mask save/restore. Lanes without a positive discriminant compute throw-away
     // values (sqrt of a negative is NaN) and are excluded by `pos` in the final select.
-    if (__ballot(mq[0] > 0.f)) {
+    if (ballot(mq[0] > 0.f)) {
         if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             const bool pos = dq[k] > 0.f;                                    // :62
-            if (__ballot(pos)) {
+            if (ballot(pos)) {
                 if (STATS) { dbg.lane_roots += pos; if (first_active_lane()) ++dbg.wave_roots; }
                 float q;
                 float t = near_root(bq[k], dq[k], rd, q);                    // :63
                 const bool ok = in_range(t);
-                if (__ballot(pos && !ok)) {
+                if (ballot(pos && !ok)) {
                     const float t2 = far_root(bq[k], q, rd);                 // :76
                     t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
                 } else {
@@ -477,11 +501,11 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
         }
         const bool pos = valid && disc > 0.f;                              // :62
         uint64_t key = ~0ull;
-        if (__ballot(pos)) {
+        if (ballot(pos)) {
             float q;
             float t = near_root(b, disc, rdr, q);                          // :63
             const bool ok = in_range(t);
-            if (__ballot(pos && !ok)) {
+            if (ballot(pos && !ok)) {
                 RT_EV(EV_T_FAR);
                 const float t2 = far_root(b, q, rdr);                      // :76
                 t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
@@ -509,7 +533,7 @@ __device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, co
                                                  const uint32_t *__restrict__ sidx, TransposeLds *tw, uint32_t tmax,
                                                  f3 o, f3 d, const RayDiv &rd, Hit &h, Dbg &dbg, WaveTally<COUNT> &wt)
 {
-    const uint64_t M = __ballot(req);
+    const uint64_t M = ballot(req);
     if (!M) return;
     RT_EV(EV_CLUSTER_REQ);
     const uint32_t scu = __builtin_amdgcn_readfirstlane(scu_lane);
@@ -553,7 +577,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         uint32_t n_supers = p.n_supers;
         if (p.use_root) {
             wt.add_box(lanes(active));
-            if (!__ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)))
+            if (!ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)))
                 n_supers = 0;
         }
         if (n_supers) RT_EV(EV_ROOT_GATE_PASS);
@@ -562,7 +586,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
             const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
             wt.add_box(lanes(active));
             const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t() * 1.002f);
-            const uint64_t spm = __ballot(sp);
+            const uint64_t spm = ballot(sp);
             if (!spm) continue;
             RT_EV(EV_SUPER_PASS);
             const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
@@ -685,7 +709,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         fc_ptr_t fc = fc_base;
         asm volatile("" : "+s"(fc));
         // ---- refill items for idle lanes and start their samples -------------------
-        uint64_t need = __ballot(!alive);
+        uint64_t need = ballot(!alive);
         bool fresh = false;
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
@@ -746,7 +770,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
             cnext += took;
-            need = __ballot(!alive);
+            need = ballot(!alive);
         }
 
         stamp(0);
@@ -840,7 +864,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             }
         }
         stamp(1);
-        if (__ballot(alive) == 0) break;  // only when the item space is exhausted
+        if (ballot(alive) == 0) break;  // only when the item space is exhausted
         RT_EV(EV_ITER);
         if (STATS && lane == 0) {
             ++dbg_iters;
@@ -1068,7 +1092,7 @@ __global__ __launch_bounds__(256) void compat_kernel(const KCompat p)
     uint32_t segs = 0, tests = 0;
     for (;;) {
         // refill: idle lanes take the next pixels of the wave's chunk (64 pixels per atomic)
-        uint64_t need = __ballot(!alive);
+        uint64_t need = ballot(!alive);
         while (need && !exhausted) {
             if (cnext >= cend) {
                 uint32_t c = 0;
@@ -1092,9 +1116,9 @@ __global__ __launch_bounds__(256) void compat_kernel(const KCompat p)
                 alive = fresh = true;
             }
             cnext += min((uint32_t)__popcll(need), avail);
-            need = __ballot(!alive);
+            need = ballot(!alive);
         }
-        if (__ballot(alive) == 0) break;
+        if (ballot(alive) == 0) break;
         if (!alive) continue;
         if (fresh) {                                        // cuda_impl.cu:345-349
             const float u = ((float)x + xs_gen(rng)) / fW;

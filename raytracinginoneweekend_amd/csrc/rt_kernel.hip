@@ -252,9 +252,10 @@ struct WaveTally {
     __device__ __forceinline__ void add_sph(uint64_t n) { if (COUNT) sph += n; }
     __device__ __forceinline__ void add_box(uint32_t n) { if (COUNT) box += n; }
 };
-// The lane mask of a predicate, straight from the compare that forms it. (HIP's __ballot takes
-// an int, so the predicate is first materialised as 0/1 in a VGPR and compared again: two extra
-// half-rate VALU operations per vote.)
+// The lane mask of a predicate. Votes are taken on single compares only: the compiler turns the
+// vote of a compare into one scalar AND with exec, but materialises any other predicate (an AND
+// of compares, a value carried across blocks) as 0/1 in a VGPR and compares it again, two extra
+// half-rate VALU operations; compound conditions are formed from masks instead.
 __device__ __forceinline__ uint64_t ballot(bool x) { return __builtin_amdgcn_ballot_w64(x); }
 __device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(ballot(x)); }
 
@@ -285,14 +286,14 @@ __device__ __forceinline__ uint64_t hit_key(float t, uint32_t id)
 // numerator's) and every discriminant is below 2^96.
 struct RayDiv {
     float a, y;  // divisor |d|^2 and its refined reciprocal
-    bool fd;     // wave-uniform: the short forms are exact for every lane
+    uint32_t fd; // wave-uniform (a scalar, not a lane predicate): the short forms are exact for every lane
 };
-__device__ __forceinline__ RayDiv ray_div(float a, bool active, uint32_t fast_roots)
+__device__ __forceinline__ RayDiv ray_div(float a, uint64_t active, uint32_t fast_roots)
 {
     const float y0 = __builtin_amdgcn_rcpf(a);
     const float y = fmaf(fmaf(-a, y0, 1.f), y0, y0);
-    const bool ok = a >= 0x1p-40f && a <= 0x1p40f;
-    return {a, y, fast_roots != 0u && !ballot(active && !ok)};
+    const uint64_t ok = ballot(a >= 0x1p-40f) & ballot(a <= 0x1p40f);  // NaN: neither
+    return {a, y, (fast_roots != 0u && !(active & ~ok)) ? 1u : 0u};
 }
 // n / a: the IEEE sequence (v_div_scale, rcp + refinement, two FMA corrections, v_div_fmas,
 // v_div_fixup) with no scaling and no special value, i.e. its two corrections
@@ -315,10 +316,18 @@ __device__ __forceinline__ float sqrt_scaled(float x)
     r = fmaf(-sup, s, xs) > 0.f ? sup : r;
     return r * 0x1p-16f;
 }
+// r.fd, re-read as a scalar at each use: left to itself the compiler hoists `fd != 0` out of the
+// sphere loops as a lane predicate and rebuilds its negation per use with two VALU operations
+__device__ __forceinline__ bool fast_div(const RayDiv &r)
+{
+    uint32_t f = __builtin_amdgcn_readfirstlane(r.fd);
+    asm volatile("" : "+s"(f));
+    return f != 0u;
+}
 // the near root (-b - sqrt(disc)) / a and its sqrt, raytracer.hxx:62-63
 __device__ __forceinline__ float near_root(float b, float disc, const RayDiv &r, float &q)
 {
-    if (r.fd) {
+    if (fast_div(r)) {
         q = sqrt_scaled(disc);
         return div_ray(-b - q, r);
     }
@@ -328,7 +337,7 @@ __device__ __forceinline__ float near_root(float b, float disc, const RayDiv &r,
 // the far root (-b + sqrt(disc)) / a, raytracer.hxx:76
 __device__ __forceinline__ float far_root(float b, float q, const RayDiv &r)
 {
-    return r.fd ? div_ray(-b + q, r) : (-b + q) / r.a;
+    return fast_div(r) ? div_ray(-b + q, r) : (-b + q) / r.a;
 }
 
 template <bool FAST, bool STATS, int N = 8>
@@ -370,12 +379,13 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             const bool pos = dq[k] > 0.f;                                    // :62
-            if (ballot(pos)) {
+            const uint64_t posm = ballot(pos);
+            if (posm) {
                 if (STATS) { dbg.lane_roots += pos; if (first_active_lane()) ++dbg.wave_roots; }
                 float q;
                 float t = near_root(bq[k], dq[k], rd, q);                    // :63
                 const bool ok = in_range(t);
-                if (ballot(pos && !ok)) {
+                if (posm & ~ballot(ok)) {
                     const float t2 = far_root(bq[k], q, rd);                 // :76
                     t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
                 } else {
@@ -478,6 +488,7 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint32_t k = lane & 15u;          // member slot (slots >= cnt read beyond: masked)
     const bool kval = k < cnt;
+    const uint64_t kvalm = ballot(kval);
     const float4 s = geo[start + k];
     const uint32_t sid = sidx[start + k];
     for (uint32_t r0 = 0; r0 < m; r0 += 4u) {
@@ -500,12 +511,15 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
             disc = b * b - ra * c;                                         // :60
         }
         const bool pos = valid && disc > 0.f;                              // :62
+        // rows of rays r < m: the first 16 (m - r0) lanes
+        const uint64_t rowm = m - r0 >= 4u ? ~0ull : (1ull << (16u * (m - r0))) - 1ull;
+        const uint64_t posm = ballot(disc > 0.f) & kvalm & rowm;
         uint64_t key = ~0ull;
-        if (ballot(pos)) {
+        if (posm) {
             float q;
             float t = near_root(b, disc, rdr, q);                          // :63
             const bool ok = in_range(t);
-            if (ballot(pos && !ok)) {
+            if (posm & ~ballot(ok)) {
                 RT_EV(EV_T_FAR);
                 const float t2 = far_root(b, q, rdr);                      // :76
                 t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
@@ -529,11 +543,11 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 template <bool FAST, bool STATS, bool COUNT>
-__device__ __forceinline__ void cluster_members7(bool req, uint32_t scu_lane, const float4 *__restrict__ geo,
+__device__ __forceinline__ void cluster_members7(bool req, uint64_t M, uint32_t scu_lane, const float4 *__restrict__ geo,
                                                  const uint32_t *__restrict__ sidx, TransposeLds *tw, uint32_t tmax,
                                                  f3 o, f3 d, const RayDiv &rd, Hit &h, Dbg &dbg, WaveTally<COUNT> &wt)
 {
-    const uint64_t M = ballot(req);
+    // req: this lane's segment reaches the cluster box; M: the wave's mask of such lanes
     if (!M) return;
     RT_EV(EV_CLUSTER_REQ);
     const uint32_t scu = __builtin_amdgcn_readfirstlane(scu_lane);
@@ -553,8 +567,9 @@ template <bool FAST, int CULL, bool STATS, bool COUNT>
 __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
                                            f3 d, const RayDiv &rd, Dbg &dbg, WaveTally<COUNT> &wt, bool active,
-                                           TransposeLds *tw)
+                                           uint64_t am, TransposeLds *tw)
 {
+    // active: this lane traces a segment; am: the wave's mask of such lanes
     Hit h{kNoHit};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
     if (CULL) {
@@ -577,7 +592,7 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
         uint32_t n_supers = p.n_supers;
         if (p.use_root) {
             wt.add_box(lanes(active));
-            if (!ballot(active && box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)))
+            if (!(ballot(box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)) & am))
                 n_supers = 0;
         }
         if (n_supers) RT_EV(EV_ROOT_GATE_PASS);
@@ -585,20 +600,22 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
             RT_EV(EV_SUPER);
             const float4 s0 = sup[2 * g], s1 = sup[2 * g + 1];
             wt.add_box(lanes(active));
-            const bool sp = active && box_pass(rb, s0, s1, t_lo, h.t() * 1.002f);
-            const uint64_t spm = ballot(sp);
+            const bool bs = box_pass(rb, s0, s1, t_lo, h.t() * 1.002f);
+            const uint64_t spm = ballot(bs) & am;
             if (!spm) continue;
+            const bool sp = bs & active;
             RT_EV(EV_SUPER_PASS);
             const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
             wt.add_box(4u * (uint32_t)__popcll(spm));
             for (uint32_t c = c0i; c < c0i + 4; c += 2) {
                 const float tb_now = h.t() * 1.002f;
                 const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
-                const bool pa = sp && box_pass(rb, a0, a1, t_lo, tb_now), pb = sp && box_pass(rb, b0, b1, t_lo, tb_now);
-                cluster_members7<FAST, STATS, COUNT>(pa, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o, d, rd, h,
-                                              dbg, wt);
-                cluster_members7<FAST, STATS, COUNT>(pb, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o, d, rd, h,
-                                              dbg, wt);
+                const bool ba = box_pass(rb, a0, a1, t_lo, tb_now), bb = box_pass(rb, b0, b1, t_lo, tb_now);
+                const uint64_t pam = ballot(ba) & spm, pbm = ballot(bb) & spm;
+                cluster_members7<FAST, STATS, COUNT>(ba & sp, pam, __float_as_uint(a1.w), geo, sidx, tw, p.transpose_max, o,
+                                                     d, rd, h, dbg, wt);
+                cluster_members7<FAST, STATS, COUNT>(bb & sp, pbm, __float_as_uint(b1.w), geo, sidx, tw, p.transpose_max, o,
+                                                     d, rd, h, dbg, wt);
             }
         }
     }
@@ -879,13 +896,14 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         // |d|^2 (raytracer.hxx:56) and its refined reciprocal for this segment's roots; the sky
         // below reuses both (unit_direction's length is sqrt of the same sum)
         const float a = d.x * d.x + d.y * d.y + d.z * d.z;
-        const RayDiv rd = ray_div(a, seg, p.fast_roots);
+        const uint64_t segm = ballot(seg);
+        const RayDiv rd = ray_div(a, segm, p.fast_roots);
         Hit h{kNoHit};
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
-            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, seg, tw);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, tw);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
-            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, true, nullptr);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr);
         }
         stamp(2);
         {
@@ -911,7 +929,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     // and d.y / length is exact unless |d.y| < 2^-100, where both forms give
                     // |y| < 2^-80 and tt rounds to 1 either way.
                     float uy;
-                    if (rd.fd) {
+                    if (rd.fd != 0u) {
                         const float l = sqrt_scaled(a);
                         const float y0 = __builtin_amdgcn_rcpf(l);
                         uy = div_ray(d.y, RayDiv{l, fmaf(fmaf(-l, y0, 1.f), y0, y0), true});

@@ -170,7 +170,7 @@ struct rt_scene {
     float clus_pad[2] = {0.f, 0.f};
     uint32_t n_supers[2] = {0, 0}, supers_offset[2] = {0, 0};
     uint32_t shade_offset[2] = {0, 0};
-    bool in_fast_range = false;  // every sphere within 2^19 of the origin (short exact root forms)
+    bool in_fast_range = false;  // every sphere within 2^19 of the origin, radii >= 2^-40 (short exact forms)
     // workspaces: consecutive render passes (of one frame or of consecutive frames) rotate over
     // internal streams xs[b] and workspaces slots[b], so a pass renders while the caller stream
     // still accumulates the previous ones
@@ -864,9 +864,12 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     rt_scene *sc = new rt_scene();
     for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
     sc->in_fast_range = true;
-    for (uint32_t i = 0; i < n_spheres; ++i)
+    for (uint32_t i = 0; i < n_spheres; ++i) {
         for (float v : {spheres[i].center[0], spheres[i].center[1], spheres[i].center[2], spheres[i].radius})
             if (!(std::fabs(v) <= 0x1p19f)) sc->in_fast_range = false;
+        // the hit normal's short division by r (rt_kernel.hip div3_short) needs |r| >= 2^-40
+        if (!(std::fabs(spheres[i].radius) >= 0x1p-40f)) sc->in_fast_range = false;
+    }
     sc->device = device;
     sc->n_spheres = n_spheres;
     sc->n_materials = n_materials;

@@ -324,6 +324,21 @@ __device__ __forceinline__ bool fast_div(const RayDiv &r)
     asm volatile("" : "+s"(f));
     return f != 0u;
 }
+// n / r for the three components of n by the short form, with r's refined reciprocal formed once.
+// The caller has checked that no operand takes the IEEE sequence's scaling or fix-up paths:
+// r in [2^-40, 2^20], every |n_i| in [2^-100, 2^21] (so no zero, whose sign the short form can
+// lose, and no quotient below 2^-126).
+__device__ __forceinline__ f3 div3_short(f3 n, float r)
+{
+    const float y0 = __builtin_amdgcn_rcpf(r);
+    const RayDiv rr{r, fmaf(fmaf(-r, y0, 1.f), y0, y0), 1u};
+    return mk(div_ray(n.x, rr), div_ray(n.y, rr), div_ray(n.z, rr));
+}
+// every active lane's |n_i| >= 2^-100 (a wave-uniform answer; one min3 and one compare per lane)
+__device__ __forceinline__ bool all_lanes_min_abs_ok(f3 n)
+{
+    return !ballot(!(fminf(fminf(fabsf(n.x), fabsf(n.y)), fabsf(n.z)) >= 0x1p-100f));
+}
 // the near root (-b - sqrt(disc)) / a and its sqrt, raytracer.hxx:62-63
 __device__ __forceinline__ float near_root(float b, float disc, const RayDiv &r, float &q)
 {
@@ -961,7 +976,13 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     }
                     const f3 ctr = mk(sf.x, sf.y, sf.z);
                     const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
-                    const f3 hn = (hp - ctr) / sf.w;            // raytracer.hxx:71
+                    // raytracer.hxx:71. With the scene in the short-form range (|r| in [2^-40, 2^19],
+                    // p.fast_roots) the division by r takes the short form unless a lane's offset has
+                    // a component below 2^-100 (zero included).
+                    const f3 dv = hp - ctr;
+                    f3 hn;
+                    if (p.fast_roots && all_lanes_min_abs_ok(dv)) hn = div3_short(dv, sf.w);
+                    else hn = dv / sf.w;
                     att = att * mk(md.x, md.y, md.z);           // main.cxx:65 (unused if absorbed)
                     // raytracer.hxx:120-199
                     o = hp;
@@ -974,7 +995,13 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                         // metal and dielectric lanes share one unit direction and one reflection
                         // (one code path for the wave instead of two)
                         RT_EV(EV_UNIT_DIR);
-                        const f3 ud = normalize(d);
+                        // unit_vector(d) (math.hxx:219-227): length sqrt(a) with a = |d|^2 as above;
+                        // under rd.fd, a in [2^-40, 2^40], so the length is sqrt_scaled(a) in
+                        // [2^-20, 2^20] and the three divisions take the short form unless a
+                        // lane's direction has a component below 2^-100
+                        f3 ud;
+                        if (rd.fd != 0u && all_lanes_min_abs_ok(d)) ud = div3_short(d, sqrt_scaled(a));
+                        else ud = normalize(d);
                         const f3 rf = reflect(ud, hn);
                         if (kind == 1u) {                       // metal, :143-156
                             d = rf;                             // + rius * roughness next iteration

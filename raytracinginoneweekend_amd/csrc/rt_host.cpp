@@ -65,6 +65,8 @@ hv hnorm(hv a)
 hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x}; }
 
 constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 GiB)
+// (the kernel forms a slot index sample * n_pixels + pixel in 32 bits)
+static_assert(kMaxSlotsBytes / 12 < (1ull << 32), "slot index width");
 // 2 x 8 queue lines, 2 x 4 u64 segment counters, then the compat kernel's pixel counter
 // internal render streams for frames in flight (RT_PIPELINE = 2..kMaxBufs), and workspaces:
 // RT_WS_PER_STREAM (1..2) per stream, at most kMaxWs

@@ -638,6 +638,12 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
 }
 
 // ---- the megakernel ----------------------------------------------------------------------
+// p[i] read from global memory, named as such (a float4 load from address space 1)
+__device__ __forceinline__ float4 gld4(const float4 *p, uint32_t i)
+{
+    const __attribute__((address_space(1))) float *g = (const __attribute__((address_space(1))) float *)(p + i);
+    return make_float4(g[0], g[1], g[2], g[3]);
+}
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
 #endif
@@ -886,7 +892,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     } else {                               // absorbed: main.cxx:68, colour 0
                         RT_EV(EV_METAL_ABSORB);
                         alive = false;
-                        float *dst = p.slots + ((size_t)ls * fc->n_pixels + pix) * 3u;
+                        float *dst = p.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
                         dst[0] = 0.f;
                         dst[1] = 0.f;
                         dst[2] = 0.f;
@@ -968,11 +974,14 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                         sf = shade[2 * ib];
                         md = shade[2 * ib + 1];
                         kind = reinterpret_cast<const uint8_t *>(shade + 2 * p.n_spheres)[ib];
+                        asm volatile("");  // keeps the LDS and global loads apart (no sinking)
                     } else {
+                        // global memory, named as such: the two branches' loads would otherwise be
+                        // merged into flat loads through a selected pointer
                         const float4 *shade = p.blob + p.shade_offset;
-                        sf = shade[2 * ib];
-                        md = shade[2 * ib + 1];
-                        kind = reinterpret_cast<const uint8_t *>(shade + 2 * p.n_spheres)[ib];
+                        sf = gld4(shade, 2 * ib);
+                        md = gld4(shade, 2 * ib + 1);
+                        kind = ((const __attribute__((address_space(1))) uint8_t *)(shade + 2 * p.n_spheres))[ib];
                     }
                     const f3 ctr = mk(sf.x, sf.y, sf.z);
                     const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
@@ -1011,8 +1020,14 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                         } else {                                // dielectric, :158-194
                             RT_EV(EV_DIELECTRIC);
                             // {1 / ior, x(ior), x(1 / ior)} of this sphere, x(r) = (1 - r) / (1 + r)
-                            const float4 dcs = (V != V_EXACT_SCALAR && p.shade_lds ? blob : p.blob)
-                                [p.shade_offset + 2 * p.n_spheres + (p.n_spheres + 15u) / 16u + ib];
+                            const uint32_t di = p.shade_offset + 2 * p.n_spheres + (p.n_spheres + 15u) / 16u + ib;
+                            float4 dcs;
+                            if (V != V_EXACT_SCALAR && p.shade_lds) {
+                                dcs = blob[di];
+                                asm volatile("");  // no merged (flat) load, as above
+                            } else {
+                                dcs = gld4(p.blob, di);
+                            }
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w, xs = dcs.y;
                             float cosv = dot(ud, hn);
@@ -1037,7 +1052,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                 // the sample's colour goes to its slot; accumulate_kernel forms the reference's
                 // blocked sum over the slots (main.cxx:205)
                 alive = false;
-                float *dst = p.slots + ((size_t)ls * fc->n_pixels + pix) * 3u;
+                float *dst = p.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
                 dst[0] = col.x;
                 dst[1] = col.y;
                 dst[2] = col.z;

@@ -387,8 +387,12 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
         for (int k = 0; k < w; ++k) mq[k] = fmaxf(mq[k], mq[k + w]);
     // Wave-uniform branches (ballots) around the root work, lane selects inside: a masked
     // lane costs the same issue slots as a computing one, and uniform branches need no
-    // exec-mask save/restore. Lanes without a positive discriminant compute throw-away
-    // values (sqrt of a negative is NaN) and are excluded by `pos` in the final select.
+    // exec-mask save/restore. Lanes without a positive discriminant take the root of -1
+    // (NaN), so their candidate is NaN, whose key never wins (NaN bits order above every
+    // finite t): no predicate is carried to the key update, which is selected by the key
+    // compare alone. (Formed as `pos && kt < h.key`, the mask would be ANDed into VCC by a
+    // scalar op, and a VALU read of a VCC that a scalar op wrote stalls ~20 cycles on gfx950,
+    // scripts/ubench_int.hip.)
     if (ballot(mq[0] > 0.f)) {
         if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
 #pragma unroll
@@ -397,8 +401,9 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
             const uint64_t posm = ballot(pos);
             if (posm) {
                 if (STATS) { dbg.lane_roots += pos; if (first_active_lane()) ++dbg.wave_roots; }
+                const float dk = pos ? dq[k] : -1.f;
                 float q;
-                float t = near_root(bq[k], dq[k], rd, q);                    // :63
+                float t = near_root(bq[k], dk, rd, q);                       // :63
                 const bool ok = in_range(t);
                 if (posm & ~ballot(ok)) {
                     const float t2 = far_root(bq[k], q, rd);                 // :76
@@ -407,7 +412,7 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
                     t = ok ? t : __builtin_nanf("");
                 }
                 const uint64_t kt = hit_key(t, sidx[i + k]);
-                if (pos && kt < h.key) h.key = kt;
+                if (kt < h.key) h.key = kt;
             }
         }
     }
@@ -502,15 +507,13 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint32_t k = lane & 15u;          // member slot (slots >= cnt read beyond: masked)
-    const bool kval = k < cnt;
-    const uint64_t kvalm = ballot(kval);
+    const float kth = k < cnt ? 0.f : __builtin_inff();  // slots past the cluster never test positive
     const float4 s = geo[start + k];
     const uint32_t sid = sidx[start + k];
     for (uint32_t r0 = 0; r0 < m; r0 += 4u) {
         RT_EV(EV_T_ROUND);
         const uint32_t r = r0 + (lane >> 4);
-        const bool valid = kval && r < m;
-        const uint32_t rr = min(r, m - 1u);
+        const uint32_t rr = min(r, m - 1u);  // rows r >= m repeat ray m - 1; their keys are not stored
         const float4 q0 = tw->ray[rr][0], q1 = tw->ray[rr][1];
         const float ra = q0.w;                                              // |d|^2, as closest_hit
         const RayDiv rdr{ra, q1.w, rd.fd};
@@ -525,14 +528,13 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
             const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;     // :58
             disc = b * b - ra * c;                                         // :60
         }
-        const bool pos = valid && disc > 0.f;                              // :62
-        // rows of rays r < m: the first 16 (m - r0) lanes
-        const uint64_t rowm = m - r0 >= 4u ? ~0ull : (1ull << (16u * (m - r0))) - 1ull;
-        const uint64_t posm = ballot(disc > 0.f) & kvalm & rowm;
+        const bool pos = disc > kth;                                       // :62
+        const uint64_t posm = ballot(pos);
         uint64_t key = ~0ull;
         if (posm) {
+            const float dk = pos ? disc : -1.f;  // NaN candidate without a positive discriminant
             float q;
-            float t = near_root(b, disc, rdr, q);                          // :63
+            float t = near_root(b, dk, rdr, q);                            // :63
             const bool ok = in_range(t);
             if (posm & ~ballot(ok)) {
                 RT_EV(EV_T_FAR);
@@ -541,7 +543,9 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
             } else {
                 t = ok ? t : __builtin_nanf("");
             }
-            if (pos && t == t) key = hit_key(t, sid);
+            // NaN keys (no candidate) lose to every valid key in the row minimum and in the
+            // owner's update, like ~0 (test_block8)
+            key = hit_key(t, sid);
         }
         key = min16_key(key);
         if (k == 0u && r < m) tw->key[r] = key;

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <utility>
+#include <cstdlib>
 
 constexpr int kIters = 16384;
 
@@ -240,13 +241,37 @@ __global__ __launch_bounds__(256) void probe(uint32_t *out, uint32_t c)
 #define X(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[i]) : "v"(v))
         if (OP == 67) C8(X)
 #undef X
+#define X(i) asm volatile("v_cmp_gt_f32 vcc, %0, %1\n\ts_nop 1\n\tv_cndmask_b32 %0, %1, %0, vcc" : "+v"(x[i]) : "v"(v) : "vcc")
+        if (OP == 68) C8(X)
+#undef X
+#define X(i) asm volatile("v_cmp_gt_f32_e64 %2, %0, %1\n\tv_cndmask_b32_e64 %0, %1, %0, %2" : "+v"(x[i]) : "v"(v), "s"(m))
+        if (OP == 69) C8(X)
+#undef X
+#define X(i) asm volatile("v_cndmask_b32_e32 %0, %1, %0, vcc" : "+v"(x[i]) : "v"(v))
+        if (OP == 70) C8(X)
+#undef X
+#define X(i) asm volatile("v_fma_f32 %0, %0, %1, 1.0\n\tv_fma_f32 %0, %0, %1, 1.0" : "+v"(x[i]) : "v"(v))
+        if (OP == 71) C8(X)
+#undef X
+#define X(i) asm volatile("s_mov_b64 vcc, %2\n\tv_cndmask_b32_e32 %0, %1, %0, vcc" : "+v"(x[i]) : "v"(v), "s"(m) : "vcc")
+        if (OP == 72) C8(X)
+#undef X
+#define X(i) asm volatile("s_mov_b64 s[40:41], %2\n\tv_cndmask_b32_e64 %0, %1, %0, s[40:41]" : "+v"(x[i]) : "v"(v), "s"(m) : "s40", "s41")
+        if (OP == 73) C8(X)
+#undef X
+#define X(i) asm volatile("v_cmp_gt_f32 vcc, %0, %1\n\ts_and_b64 vcc, vcc, exec\n\tv_cndmask_b32 %0, %1, %0, vcc" : "+v"(x[i]) : "v"(v) : "vcc")
+        if (OP == 74) C8(X)
+#undef X
+#define X(i) asm volatile("v_cmp_gt_f32_e64 s[40:41], %0, %1\n\ts_and_b64 s[40:41], s[40:41], exec\n\tv_cndmask_b32_e64 %0, %1, %0, s[40:41]" : "+v"(x[i]) : "v"(v) : "s40", "s41")
+        if (OP == 75) C8(X)
+#undef X
     }
     uint32_t r = (uint32_t)m;
     for (int i = 0; i < 8; ++i) r ^= x[i] ^ (uint32_t)y[i] ^ (uint32_t)(y[i] >> 32);
     out[blockIdx.x * 256 + threadIdx.x] = r;
 }
 
-constexpr int kOps = 68;
+constexpr int kOps = 76;
 const char *kNames[kOps] = {
     "v_fma_f32 v,v,v",     "v_fma_f32 v,s,v",      "v_mul_f32 lit,v"  ,       "v_fma_f32 v,2.0,v",
     "v_cndmask vcc",       "v_cndmask_e64 s[]",    "v_cmp_lt_f32 vcc",        "v_cmp_lt_f32_e64 s[]",
@@ -257,7 +282,9 @@ const char *kNames[kOps] = {
     "v_mul_hi_u32 v,v",    "v_max_f32 v,v",        "v_sub_f32 v,v",           "v_med3_f32",
     "v_lshlrev_b64",       "v_lshl_add_u32",       "v_fma_f64",               "v_mul_f64",
     "v_cvt_f64_f32",       "v_rcp_f32",            "v_sqrt_f32",              "v_cndmask_e64 0,s[]",
-    "v_and_b32 v,v", "v_or_b32 v,v", "v_sub_u32 v,v", "v_lshlrev_b32 3,v", "v_lshrrev_b32 v,v", "v_bfe_u32", "v_mul_u32_u24 v,v", "v_min_u32 v,v", "v_max_i32 v,v", "v_fmac_f32 v,v", "v_mov_b32 v,v", "v_mov_b32 v,lit", "v_not_b32", "v_bfi_b32", "v_perm_b32", "v_cvt_f32_i32", "v_ldexp_f32 v,v", "v_cmp_class_f32", "v_cmp_lt_u32 vcc", "v_add_co_u32 vcc", "v_sub_f32 clamp", "v_mul_f32 neg/abs", "v_add_f32_dpp", "v_max3_f32", "v_or3_b32", "v_lshl_or_b32", "v_pk_mul_f32", "v_pk_add_f32", "v_exp_f32", "v_frexp_mant_f32", "v_div_fixup_f32", "v_cndmask vcc (no clobber)"};
+    "v_and_b32 v,v", "v_or_b32 v,v", "v_sub_u32 v,v", "v_lshlrev_b32 3,v", "v_lshrrev_b32 v,v", "v_bfe_u32", "v_mul_u32_u24 v,v", "v_min_u32 v,v", "v_max_i32 v,v", "v_fmac_f32 v,v", "v_mov_b32 v,v", "v_mov_b32 v,lit", "v_not_b32", "v_bfi_b32", "v_perm_b32", "v_cvt_f32_i32", "v_ldexp_f32 v,v", "v_cmp_class_f32", "v_cmp_lt_u32 vcc", "v_add_co_u32 vcc", "v_sub_f32 clamp", "v_mul_f32 neg/abs", "v_add_f32_dpp", "v_max3_f32", "v_or3_b32", "v_lshl_or_b32", "v_pk_mul_f32", "v_pk_add_f32", "v_exp_f32", "v_frexp_mant_f32", "v_div_fixup_f32", "v_cndmask vcc (no clobber)",
+    "cmp vcc + cndmask vcc (pair)", "cmp s[] + cndmask s[] (pair)", "cndmask_e32 vcc, no clobber", "fma pair (reference)",
+    "s_mov vcc + cndmask_e32 vcc", "s_mov s[] + cndmask_e64 s[]", "cmp vcc + s_and vcc + cndmask vcc", "cmp s[] + s_and s[] + cndmask_e64"};
 
 template <int OP>
 static float run(uint32_t *out, int blocks)
@@ -278,12 +305,19 @@ static float run(uint32_t *out, int blocks)
 }
 
 template <int... I>
-static void run_all(uint32_t *out, int blocks, float *ms, std::integer_sequence<int, I...>)
+static void run_all(uint32_t *out, int blocks, float *ms, int first, double insts, int clk,
+                    std::integer_sequence<int, I...>)
 {
-    ((ms[I] = run<I>(out, blocks)), ...);
+    // one line per op as it completes (a slow shape shows up before the rest)
+    ((I >= first ? (ms[I] = run<I>(out, blocks),
+                    printf("%-32s %.3f ms  %.2f cycles/wave-inst/SIMD at %.0f MHz\n", kNames[I], ms[I],
+                           ms[I] * 1e-3 * clk * 1e3 / insts, clk / 1e3),
+                    fflush(stdout), 0)
+                 : 0),
+     ...);
 }
 
-int main()
+int main(int argc, char **argv)
 {
     int clk = 0, cus = 0;
     (void)hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
@@ -292,11 +326,8 @@ int main()
     uint32_t *out;
     (void)hipMalloc(&out, sizeof(uint32_t) * 256 * blocks);
     float ms[kOps];
-    run_all(out, blocks, ms, std::make_integer_sequence<int, kOps>{});
     const double insts = 8.0 * kIters * 8;  // per SIMD: waves x iterations x chains
-    for (int i = 0; i < kOps; ++i)
-        printf("%-24s %.3f ms  %.2f cycles/wave-inst/SIMD at %.0f MHz\n", kNames[i], ms[i],
-               ms[i] * 1e-3 * clk * 1e3 / insts, clk / 1e3);
+    run_all(out, blocks, ms, argc > 1 ? atoi(argv[1]) : 0, insts, clk, std::make_integer_sequence<int, kOps>{});
     (void)hipFree(out);
     return 0;
 }

@@ -76,6 +76,13 @@ static_assert(EV_COUNT <= kDbgEvents, "event counters");
         if (STATS && first_active_lane()) ++dbg.ev[(e)]; \
     } while (0)
 
+// The lane mask of a predicate. Votes are taken on single compares only: the compiler turns the
+// vote of a compare into one scalar AND with exec, but materialises any other predicate (an AND
+// of compares, a value carried across blocks) as 0/1 in a VGPR and compares it again, two extra
+// half-rate VALU operations; compound conditions are formed from masks instead.
+__device__ __forceinline__ uint64_t ballot(bool x) { return __builtin_amdgcn_ballot_w64(x); }
+__device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(ballot(x)); }
+
 // ---- RNG: PCG32 XSH-RR per (pixel, sample) stream; the increment is wave-uniform ---------
 constexpr uint64_t kPcgMul = 6364136223846793005ULL;
 __device__ __forceinline__ uint32_t pcg_out(uint64_t old)
@@ -252,13 +259,6 @@ struct WaveTally {
     __device__ __forceinline__ void add_sph(uint64_t n) { if (COUNT) sph += n; }
     __device__ __forceinline__ void add_box(uint32_t n) { if (COUNT) box += n; }
 };
-// The lane mask of a predicate. Votes are taken on single compares only: the compiler turns the
-// vote of a compare into one scalar AND with exec, but materialises any other predicate (an AND
-// of compares, a value carried across blocks) as 0/1 in a VGPR and compares it again, two extra
-// half-rate VALU operations; compound conditions are formed from masks instead.
-__device__ __forceinline__ uint64_t ballot(bool x) { return __builtin_amdgcn_ballot_w64(x); }
-__device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(ballot(x)); }
-
 // t in (kMIN, kMAX), the reference's test (raytracer.hxx:63-64,76-77): positive binary32 values
 // are ordered as their bit patterns, and as unsigned integers every negative value and every
 // NaN lies outside the open interval of patterns, so one subtract and one compare decide it.
@@ -592,9 +592,9 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
     Hit h{kNoHit};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
     if (CULL) {
-        auto safe_rcp = [](float x) {
-            return __builtin_amdgcn_rcpf(fabsf(x) < 1e-30f ? copysignf(1e-30f, x) : x);
-        };
+        // 1/x with its magnitude clamped to 1e30 (one med3; |x| < 1e-30 behaves as 1e-30 of
+        // the same sign, zeros included): products with coordinates stay finite
+        auto safe_rcp = [](float x) { return __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(x), -1e30f, 1e30f); };
         const float ix = safe_rcp(d.x), iy = safe_rcp(d.y), iz = safe_rcp(d.z);
         const float oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
         const float aix = fabsf(ix), aiy = fabsf(iy), aiz = fabsf(iz);

@@ -567,6 +567,9 @@ int check_params(const rt_params *p)
 {
     if (!p) return fail(RT_ERR_INVALID, "params: null");
     if (!p->width || !p->height || !p->spp) return fail(RT_ERR_INVALID, "params: width, height and spp must be > 0");
+    // the kernel forms the pixel index y W + x in 32 bits (sample streams' keys)
+    if (static_cast<uint64_t>(p->width) * p->height >= (1ull << 32))
+        return fail(RT_ERR_INVALID, "params: width * height must be below 2^32");
     const uint32_t st = p->row_stride ? p->row_stride : 1;
     const uint32_t rows = rows_of(*p);
     if (rows && static_cast<uint64_t>(p->row_offset) + static_cast<uint64_t>(rows - 1) * st >= p->height)

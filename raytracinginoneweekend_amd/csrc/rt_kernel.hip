@@ -826,10 +826,14 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             pixel_of(*fc, pix, px, rr);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
             const uint32_t s = fc->sample_begin + ls;
-            const uint64_t key = ((uint64_t)py * fc->W + px) * fc->spp + s;
+            // key = (y W + x) spp + s (y W + x < 2^32: the host bounds W H)
+            const uint64_t key = (uint64_t)(py * fc->W + px) * fc->spp + s;
             const uint64_t inc_cam = ((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo;
-            rng = pcg_seed(key, inc_data);
-            rc = pcg_seed(key, inc_cam);
+            // pcg_seed(key, inc) = (inc + key) M + inc = key M + inc (M + 1): one vector multiply
+            // for both streams, the inc (M + 1) terms are wave-uniform (scalar)
+            const uint64_t km = key * kPcgMul;
+            rng = km + inc_data * (kPcgMul + 1u);
+            rc = km + inc_cam * (kPcgMul + 1u);
             const float fW = fc->fW, fH = fc->fH, rW = fc->rW, rH = fc->rH;
             const bool fw = fc->div_fast & 1u, fh = fc->div_fast & 2u;
             const float u = div_const((float)px, fW, rW, fw);

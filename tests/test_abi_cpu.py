@@ -84,6 +84,9 @@ def test_invalid_arguments_fail_loudly():
         rt.render_f32((s, m), rt.make_params(10, 10, 0))
     with pytest.raises(rt.RtError):  # rows past the bottom of the image
         rt.render_f32((s, m), rt.make_params(10, 10, 1, row_offset=5, num_rows=6))
+    with pytest.raises(rt.RtError) as e:  # pixel index y W + x must fit 32 bits (sample keys)
+        rt.render_f32((s, m), rt.make_params(1 << 16, 1 << 16, 1, num_rows=1))
+    assert e.value.status == abi.RT_ERR_INVALID and "2^32" in str(e.value)
     bad = s.copy()
     bad["material"][0] = 99
     with pytest.raises(rt.RtError) as e:

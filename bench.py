@@ -63,9 +63,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--camera", default="reference", choices=["reference", "corrected"])
-    ap.add_argument("--variant", default="exact", choices=["exact", "fast", "scalar"],
+    ap.add_argument("--variant", default="exact", choices=["exact", "fast", "scalar", "wavefront"],
                     help="exact: bit-exact kernel; fast: FMA kernel within the stated tolerance; "
-                         "scalar: brute-force scalar-cache A/B")
+                         "scalar: brute-force scalar-cache A/B; wavefront: per-segment launches with HBM ray queues "
+                         "(A/B, bit-exact)")
     ap.add_argument("--traversal", default="cull", choices=["cull", "brute"],
                     help="cull: exact cluster culling (same bits); brute: every sphere, as the reference")
     ap.add_argument("--seed", type=int, default=1234)
@@ -232,7 +233,8 @@ def main():
     rehearse = args.rehearse_world if world == 1 and args.rehearse_world > 1 else 0
     params = rank_params(W, H, spp, rehearse or world, rank, max_depth=depth, seed=args.seed,
                          scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast",
-                         brute_force=args.traversal == "brute", cuda_compat=compat)
+                         brute_force=args.traversal == "brute", cuda_compat=compat,
+                         wavefront=args.variant == "wavefront")
     rows = params.num_rows
     dev = torch.device("cuda", local)
     ds = rt.DeviceScene(arrays, device=local)
@@ -390,7 +392,7 @@ def main():
                 "per_launch_span_achieved": r3(main_m["span_achieved"]),
             },
         }
-        v = {"exact": 0, "scalar": 1, "fast": 2}[args.variant]
+        v = {"exact": 0, "scalar": 1, "fast": 2, "wavefront": 0}[args.variant]
         cull = 0 if args.traversal == "brute" or v == 1 else 7
         kname = f"render_kernel<{v}, {cull}, false, false>"
         pmc, status = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,

@@ -97,8 +97,12 @@ enum rt_flags {
     RT_FLAG_FAST_MATH = 1u << 1,  /* FMA-contracted kernel, stated tolerance          */
     RT_FLAG_SCALAR_SCENE = 1u << 2, /* A/B: brute force, spheres via the scalar cache   */
     RT_FLAG_BRUTE_FORCE = 1u << 3,  /* test every sphere (no cluster culling); same bits */
-    RT_FLAG_CUDA_COMPAT = 1u << 4   /* semantics of the reference's CUDA variant instead of its
+    RT_FLAG_CUDA_COMPAT = 1u << 4,  /* semantics of the reference's CUDA variant instead of its
                                        CPU path: src/CUDA/cuda_impl.cu (see rt_render_cuda_impl) */
+    RT_FLAG_WAVEFRONT = 1u << 5     /* A/B: the wavefront variant (one launch per segment, ray
+                                       queues in HBM) instead of the persistent megakernel;
+                                       same bits, cluster culling; RT_WAVE_QUEUE_RAYS bounds a
+                                       chunk (default 2^25 rays, 52 B each, two queues)          */
 };
 typedef struct rt_params {
     uint32_t width, height;

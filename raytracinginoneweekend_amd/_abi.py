@@ -25,6 +25,7 @@ RT_FLAG_FAST_MATH = 1 << 1
 RT_FLAG_SCALAR_SCENE = 1 << 2
 RT_FLAG_BRUTE_FORCE = 1 << 3
 RT_FLAG_CUDA_COMPAT = 1 << 4  # semantics of src/CUDA/cuda_impl.cu
+RT_FLAG_WAVEFRONT = 1 << 5  # A/B: per-segment launches with HBM ray queues (same bits)
 
 
 class RtSphere(C.Structure):

@@ -118,6 +118,21 @@ struct KCompat {
     unsigned long long *segments;  // optional [3]: segments, sphere tests, 0
 };
 
+// The wavefront variant's ray queue (structure of arrays, capacity cap rays): f = [9][cap]
+// floats {o.xyz, d.xyz, attenuation.xyz}, then the data-stream state, the item index (slot) and
+// the segment count of each ray; count = rays in the queue.
+struct RayQueue {
+    float *f;
+    uint64_t *rng;
+    uint32_t *item, *depth, *count;
+};
+struct KWave {
+    KParams p;
+    RayQueue in, out;        // wave_gen_kernel writes `out`; wave_bounce_kernel reads `in`
+    uint32_t cap;            // queue capacity (rays)
+    uint32_t item_begin, n_chunk;  // wave_gen_kernel: items [item_begin, item_begin + n_chunk)
+};
+
 // queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise
 constexpr uint32_t kQueueStride = 64;
 

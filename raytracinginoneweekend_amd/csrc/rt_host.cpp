@@ -30,6 +30,9 @@ hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid,
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream);
+hipError_t launch_wave_gen(const KWave &w, hipStream_t stream);
+hipError_t launch_wave_bounce(int cull, const KWave &w, uint32_t grid, hipStream_t stream);
+hipError_t occupancy_wave_bounce(int cull, int *blocks_per_cu, size_t lds);
 hipError_t occupancy_compat(int *blocks_per_cu);
 hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_t stream);
 } // namespace rt
@@ -77,6 +80,14 @@ constexpr uint32_t kMaxWs = 2 * kMaxBufs;
 constexpr size_t kSegWords = kMaxWs * 8 * rt::kQueueStride;
 constexpr size_t kCompatCtr = kSegWords + kMaxWs * 8 + 16;
 constexpr size_t kCtrWords = kCompatCtr + rt::kQueueStride;
+
+// RT_WAVE_QUEUE_RAYS: rays per chunk of the wavefront variant (default 2^25: 2 x 1.7 GB queues)
+uint64_t wave_queue_env()
+{
+    const char *e = std::getenv("RT_WAVE_QUEUE_RAYS");
+    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
+    return v ? std::max<uint64_t>(v, 64) : (1ull << 25);
+}
 
 // RT_SLOT_BUDGET_BYTES lowers the per-pass slot workspace (tests force multi-pass renders).
 uint64_t slot_budget()
@@ -180,6 +191,9 @@ struct rt_scene {
     size_t slots_bytes[kMaxWs] = {};
     float *acc = nullptr;
     size_t acc_bytes = 0;
+    void *wq = nullptr;  // RT_FLAG_WAVEFRONT: two ray queues and their counters
+    size_t wq_bytes = 0;
+    int occ_wave[2] = {-1, -1};  // wave_bounce_kernel blocks per CU [culled], -1 = unknown
     uint32_t *queue_ctr = nullptr;  // kCtrWords: queue and segment counters (layout at kCtrWords)
     hipStream_t xs[kMaxBufs] = {};
     hipEvent_t ev_done[kMaxWs] = {}, ev_free[kMaxWs] = {};
@@ -574,7 +588,8 @@ int check_params(const rt_params *p)
     const uint32_t rows = rows_of(*p);
     if (rows && static_cast<uint64_t>(p->row_offset) + static_cast<uint64_t>(rows - 1) * st >= p->height)
         return fail(RT_ERR_INVALID, "params: rows exceed the image height");
-    if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE | RT_FLAG_BRUTE_FORCE | RT_FLAG_CUDA_COMPAT))
+    if (p->flags & ~(RT_FLAG_FULL_FRAME | RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE | RT_FLAG_BRUTE_FORCE | RT_FLAG_CUDA_COMPAT |
+                     RT_FLAG_WAVEFRONT))
         return fail(RT_ERR_INVALID, "params: unknown flag");
     return RT_OK;
 }
@@ -804,7 +819,7 @@ int rt_scene_destroy(rt_scene *sc)
         if (sc->ev_free[b]) (void)hipEventDestroy(sc->ev_free[b]);
     }
     if (sc->ev_tail) (void)hipEventDestroy(sc->ev_tail);
-    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr})
+    for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr, sc->wq})
         if (p) (void)hipFree(p);
     for (float *p : sc->slots)
         if (p) (void)hipFree(p);
@@ -1010,12 +1025,17 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // asked for; the scalar-cache A/B variant is brute force only. Each needs its blob in LDS.
     int variant = (P.flags & RT_FLAG_FAST_MATH) ? rt::V_FAST_LDS : rt::V_EXACT_LDS;
     bool cull = !(P.flags & RT_FLAG_BRUTE_FORCE) && sc->n_clusters[1] > 0;
+    const bool wave = (P.flags & RT_FLAG_WAVEFRONT) != 0u;
+    if (wave && (P.flags & (RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE)))
+        return fail(RT_ERR_UNSUPPORTED, "rt_render_device: the wavefront variant is the exact kernel only");
     if (P.flags & RT_FLAG_SCALAR_SCENE) { variant = rt::V_EXACT_SCALAR; cull = false; }
     if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->shade_offset[cull]) * 16u > sc->max_lds) {
         if (variant == rt::V_FAST_LDS || cull) return fail(RT_ERR_UNSUPPORTED, "rt_render_device: scene too large for LDS");
         variant = rt::V_EXACT_SCALAR;
     }
-    if (variant == rt::V_EXACT_LDS && debug_stats()) {
+    if (wave && variant != rt::V_EXACT_LDS)
+        return fail(RT_ERR_UNSUPPORTED, "rt_render_device: the wavefront variant needs the scene in LDS");
+    if (variant == rt::V_EXACT_LDS && debug_stats() && !wave) {
         variant = rt::V_STATS_LDS;
         if (!sc->dbg) {
             RT_HIP(hipMalloc((void **)&sc->dbg, rt::kDbgWords * sizeof(unsigned long long)));
@@ -1074,7 +1094,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // work that last read workspace w (the accumulation of pass p - n_ws); render kernels
     // touch no caller memory, so the caller stream sees the same results in the same order.
     // RT_PIPELINE=0: everything on the caller stream.
-    const uint32_t bufs = pipeline_env();
+    const uint32_t bufs = wave ? 1u : pipeline_env();  // the wavefront variant: caller stream only
     const bool pipe = bufs > 1;
     const uint32_t n_ws = pipe ? bufs * ws_per_stream_env() : 1u;
     if (spp_pass < P.spp)
@@ -1083,6 +1103,32 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc)
             return rc;
     k.chunk_items = chunk_items();
+    // wavefront variant: two ray queues of cap rays (52 B each) and their counters
+    uint32_t wcap = 0;
+    rt::RayQueue wqa{}, wqb{};
+    int wgrid = 0;
+    if (wave) {
+        wcap = static_cast<uint32_t>(std::min<uint64_t>(n_pixels * std::min<uint64_t>(spp_pass, P.spp), wave_queue_env()));
+        const size_t qbytes = static_cast<size_t>(wcap) * 52u;
+        if (int rc = ensure(&sc->wq, &sc->wq_bytes, 2 * qbytes + 512); rc) return rc;
+        auto carve = [&](char *base, rt::RayQueue &q) {
+            q.f = reinterpret_cast<float *>(base);
+            q.rng = reinterpret_cast<uint64_t *>(base + static_cast<size_t>(wcap) * 36u);
+            q.item = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(wcap) * 44u);
+            q.depth = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(wcap) * 48u);
+        };
+        char *w0 = static_cast<char *>(sc->wq);
+        carve(w0, wqa);
+        carve(w0 + qbytes, wqb);
+        wqa.count = reinterpret_cast<uint32_t *>(w0 + 2 * qbytes);
+        wqb.count = reinterpret_cast<uint32_t *>(w0 + 2 * qbytes + 256);
+        int &ow = sc->occ_wave[cull ? 1 : 0];
+        if (ow < 0) {
+            RT_HIP(rt::occupancy_wave_bounce(cull_mode, &ow, lds));
+            ow = std::max(ow, 1);
+        }
+        wgrid = ow * sc->cu_count;
+    }
 
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
@@ -1126,7 +1172,29 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                          variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1,
                          k.guided_l2b < 0.f ? "guided log2(beta)*1e6=" : "chunk=",
                          k.guided_l2b < 0.f ? static_cast<uint32_t>(-k.guided_l2b * 1e6f) : k.chunk_items);
-        RT_HIP(rt::launch_render(variant, cull_mode, k, grid, xst));
+        if (wave) {
+            // items in chunks of wcap: one generation launch, then max_depth bounce launches
+            // (each takes every ray of its input queue; continuing rays go to the other queue)
+            rt::KWave w{};
+            w.p = k;
+            w.cap = wcap;
+            for (uint32_t c0 = 0; c0 < k.n_items; c0 += wcap) {
+                w.item_begin = c0;
+                w.n_chunk = std::min(wcap, k.n_items - c0);
+                w.out = wqa;
+                RT_HIP(rt::launch_wave_gen(w, xst));
+                rt::RayQueue qi = wqa, qo = wqb;
+                for (uint32_t b = 0; b < std::max(1u, P.max_depth); ++b) {
+                    RT_HIP(hipMemsetAsync(qo.count, 0, sizeof(uint32_t), xst));
+                    w.in = qi;
+                    w.out = qo;
+                    RT_HIP(rt::launch_wave_bounce(cull_mode, w, static_cast<uint32_t>(wgrid), xst));
+                    std::swap(qi, qo);
+                }
+            }
+        } else {
+            RT_HIP(rt::launch_render(variant, cull_mode, k, grid, xst));
+        }
         if (variant == rt::V_STATS_LDS) sc->dbg_waves = grid * 4u;
         if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], xst));
         if (pipe) {

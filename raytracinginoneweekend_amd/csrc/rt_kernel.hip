@@ -1357,6 +1357,218 @@ __global__ __launch_bounds__(256) void epilogue_rgb8_kernel(const float *in, uin
     out[i] = (uint8_t)(255.f * (float)pow((double)in[i], g));
 }
 
+// ---- the wavefront variant (RT_FLAG_WAVEFRONT; SURVEY §8(f3), an A/B against the megakernel) ----
+// Paths advance one segment per launch through ray queues in HBM: wave_gen_kernel starts one
+// sample per thread (jitter, lens) and writes its ray to queue A; wave_bounce_kernel takes every
+// ray of its input queue, finds the closest hit (the same culled walk and transposed member
+// tests), shades it, stores finished samples to their slots and appends continuing rays to its
+// output queue (one atomic per wave); the host swaps the queues max_depth times per chunk of
+// items. Rejection loops run to acceptance in the thread that needs them (no deferral), so
+// every stream sees the same draws in the same order as in the megakernel: same bits.
+__global__ __launch_bounds__(256) void wave_gen_kernel(const KWave w)
+{
+    const KParams &p = w.p;
+    const FrameConsts &fc = p.fc;
+    const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+    if (gid >= w.n_chunk) return;
+    const uint32_t I = w.item_begin + gid;
+    const uint32_t ls = udiv(I, fc.div_n_pixels.m, fc.div_n_pixels.l);
+    const uint32_t pix = I - ls * fc.n_pixels;
+    uint32_t px, rr;
+    pixel_of(fc, pix, px, rr);
+    const uint32_t py = fc.row_offset + rr * fc.row_stride;
+    const uint32_t sm = fc.sample_begin + ls;
+    const uint64_t inc_data = ((uint64_t)fc.inc_data_hi << 32) | fc.inc_data_lo;
+    const uint64_t inc_cam = ((uint64_t)fc.inc_cam_hi << 32) | fc.inc_cam_lo;
+    const uint64_t km = ((uint64_t)(py * fc.W + px) * fc.spp + sm) * kPcgMul;  // pcg_seed, as render_kernel
+    uint64_t rng = km + inc_data * (kPcgMul + 1u);
+    uint64_t rc = km + inc_cam * (kPcgMul + 1u);
+    const bool fw = fc.div_fast & 1u, fh = fc.div_fast & 2u;
+    const float u = div_const((float)px, fc.fW, fc.rW, fw);
+    const float v = div_const((float)py, fc.fH, fc.rH, fh);
+    const float uu = u + div_const(canonical(rng, inc_data), fc.fW, fc.rW, fw);
+    const float vv = v + div_const(canonical(rng, inc_data), fc.fH, fc.rH, fh);
+    const f3 r = random_in_unit_sphere(rc, inc_cam);  // camera.hxx:52
+    const f3 rd = r * fc.lens;                        // camera.hxx:46-57
+    const f3 off = mk(uu * rd.x, vv * rd.y, 0.f);
+    const f3 org = mk(fc.org[0], fc.org[1], fc.org[2]);
+    const f3 o = org + off;
+    f3 d = ((mk(fc.llc[0], fc.llc[1], fc.llc[2]) + mk(fc.hor[0], fc.hor[1], fc.hor[2]) * uu) +
+            mk(fc.ver[0], fc.ver[1], fc.ver[2]) * (1.f - vv)) - off;
+    if (fc.corrected) d = d - org;
+    const RayQueue &q = w.out;
+    q.f[0 * w.cap + gid] = o.x; q.f[1 * w.cap + gid] = o.y; q.f[2 * w.cap + gid] = o.z;
+    q.f[3 * w.cap + gid] = d.x; q.f[4 * w.cap + gid] = d.y; q.f[5 * w.cap + gid] = d.z;
+    q.f[6 * w.cap + gid] = 1.f; q.f[7 * w.cap + gid] = 1.f; q.f[8 * w.cap + gid] = 1.f;
+    q.rng[gid] = rng;
+    q.item[gid] = I;
+    q.depth[gid] = 0u;
+    if (gid == 0) *q.count = w.n_chunk;
+}
+
+template <int CULL, bool COUNT>
+__global__ __launch_bounds__(256, 6) void wave_bounce_kernel(const KWave w)
+{
+    const KParams &p = w.p;
+    extern __shared__ float4 lds_blob[];
+    for (uint32_t i = threadIdx.x; i < p.lds_units; i += blockDim.x) lds_blob[i] = p.blob[i];
+    __syncthreads();
+    const float4 *blob = lds_blob;
+    const float4 *geo = blob;
+    const uint32_t *sidx = reinterpret_cast<const uint32_t *>(blob + p.n_geo);
+    const float4 *clus = blob + p.clus_offset;
+    __shared__ TransposeLds s_tw[4];
+    TransposeLds *tw = &s_tw[threadIdx.x >> 6];
+    const uint64_t inc_data = ((uint64_t)p.fc.inc_data_hi << 32) | p.fc.inc_data_lo;
+    const RayQueue &qi = w.in, &qo = w.out;
+    const uint32_t n = *qi.count;
+    const uint32_t cap = w.cap;
+    WaveTally<COUNT> wt;
+    Dbg dbg{};
+    // whole waves walk the queue together (the cluster walk is whole-wave code)
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+        const uint32_t j = base + threadIdx.x;
+        const bool live = j < n;
+        const uint32_t jj = live ? j : 0u;
+        f3 o = mk(qi.f[0 * cap + jj], qi.f[1 * cap + jj], qi.f[2 * cap + jj]);
+        f3 d = mk(qi.f[3 * cap + jj], qi.f[4 * cap + jj], qi.f[5 * cap + jj]);
+        f3 att = mk(qi.f[6 * cap + jj], qi.f[7 * cap + jj], qi.f[8 * cap + jj]);
+        uint64_t rng = qi.rng[jj];
+        const uint32_t I = qi.item[jj];
+        uint32_t depth = qi.depth[jj];
+        const bool seg = live && depth < p.max_depth;  // main.cxx:74
+        const float a = d.x * d.x + d.y * d.y + d.z * d.z;
+        const uint64_t segm = ballot(seg);
+        const RayDiv rd = ray_div(a, segm, p.fast_roots);
+        Hit h = closest_hit<false, CULL, false, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, CULL ? tw : nullptr);
+        if (!seg) h = Hit{kNoHit};
+        {
+            const uint32_t ns = lanes(seg);
+            wt.add_seg(ns);
+            wt.add_sph((uint64_t)ns * p.n_always);
+        }
+        bool done = false, cont = false;
+        f3 col = mk(0.f, 0.f, 0.f);
+        if (live) {
+            if (!seg) {
+                done = true;
+            } else {
+                const float t = h.t();
+                const uint32_t ib = h.id();
+                ++depth;
+                if (ib == 0xffffffffu) {  // main.cxx:71, as render_kernel
+                    float uy;
+                    if (rd.fd != 0u) {
+                        const float l = sqrt_scaled(a);
+                        const float y0 = __builtin_amdgcn_rcpf(l);
+                        uy = div_ray(d.y, RayDiv{l, fmaf(fmaf(-l, y0, 1.f), y0, y0), 1u});
+                    } else {
+                        uy = normalize(d).y;
+                    }
+                    const float tt = .5f * uy + 1.f;
+                    const f3 bg = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
+                    col = bg * att;
+                    done = true;
+                } else if (depth >= p.max_depth) {
+                    done = true;
+                } else {
+                    float4 sf, md;
+                    uint32_t kind;
+                    if (p.shade_lds) {
+                        const float4 *shade = blob + p.shade_offset;
+                        sf = shade[2 * ib];
+                        md = shade[2 * ib + 1];
+                        kind = reinterpret_cast<const uint8_t *>(shade + 2 * p.n_spheres)[ib];
+                        asm volatile("");
+                    } else {
+                        const float4 *shade = p.blob + p.shade_offset;
+                        sf = gld4(shade, 2 * ib);
+                        md = gld4(shade, 2 * ib + 1);
+                        kind = ((const __attribute__((address_space(1))) uint8_t *)(shade + 2 * p.n_spheres))[ib];
+                    }
+                    const f3 hp = o + d * t;  // math.hxx:353
+                    const f3 dv = hp - mk(sf.x, sf.y, sf.z);
+                    f3 hn;
+                    if (p.fast_roots && all_lanes_min_abs_ok(dv)) hn = div3_short(dv, sf.w);
+                    else hn = dv / sf.w;  // raytracer.hxx:71
+                    att = att * mk(md.x, md.y, md.z);
+                    o = hp;
+                    cont = true;
+                    if (kind == 0u) {  // lambert, raytracer.hxx:132-141
+                        const f3 pn = hp + hn;
+                        const f3 r = random_in_unit_sphere(rng, inc_data);
+                        d = (pn + r) - hp;
+                    } else {
+                        f3 ud;
+                        if (rd.fd != 0u && all_lanes_min_abs_ok(d)) ud = div3_short(d, sqrt_scaled(a));
+                        else ud = normalize(d);
+                        const f3 rf = reflect(ud, hn);
+                        if (kind == 1u) {  // metal, :143-156
+                            const f3 r = random_in_unit_sphere(rng, inc_data);
+                            const f3 nd = rf + r * md.w;
+                            if (dot(nd, hn) > 0.f) {
+                                d = nd;
+                            } else {  // absorbed: main.cxx:68, colour 0
+                                cont = false;
+                                done = true;
+                            }
+                        } else {  // dielectric, :158-194
+                            const uint32_t di = p.shade_offset + 2 * p.n_spheres + (p.n_spheres + 15u) / 16u + ib;
+                            float4 dcs;
+                            if (p.shade_lds) {
+                                dcs = blob[di];
+                                asm volatile("");
+                            } else {
+                                dcs = gld4(p.blob, di);
+                            }
+                            f3 outward = mk(-hn.x, -hn.y, -hn.z);
+                            float ri = md.w, xs = dcs.y;
+                            float cosv = dot(ud, hn);
+                            if (cosv <= 0.f) {
+                                outward = outward * -1.f;
+                                ri = dcs.x;
+                                xs = dcs.z;
+                                cosv *= -1.f;
+                            }
+                            const f3 refr = refract(ud, outward, ri);
+                            float prob = 1.f;
+                            if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick_x(xs, cosv);
+                            d = canonical(rng, inc_data) < prob ? rf : refr;
+                        }
+                    }
+                }
+            }
+        }
+        if (done) {
+            float *dst = p.slots + (size_t)I * 3u;
+            dst[0] = col.x;
+            dst[1] = col.y;
+            dst[2] = col.z;
+        }
+        // continuing rays: one atomic per wave, ranks by mbcnt
+        const uint64_t cm = ballot(cont);
+        if (cm) {
+            uint32_t b0 = 0;
+            if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(cm)) b0 = atomicAdd(qo.count, (uint32_t)__popcll(cm));
+            b0 = __builtin_amdgcn_readlane(b0, __builtin_ctzll(cm));
+            if (cont) {
+                const uint32_t k = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+                qo.f[0 * cap + k] = o.x; qo.f[1 * cap + k] = o.y; qo.f[2 * cap + k] = o.z;
+                qo.f[3 * cap + k] = d.x; qo.f[4 * cap + k] = d.y; qo.f[5 * cap + k] = d.z;
+                qo.f[6 * cap + k] = att.x; qo.f[7 * cap + k] = att.y; qo.f[8 * cap + k] = att.z;
+                qo.rng[k] = rng;
+                qo.item[k] = I;
+                qo.depth[k] = depth;
+            }
+        }
+    }
+    if (COUNT && p.segments && (threadIdx.x & 63u) == 0u) {
+        atomicAdd(p.segments + 0, (unsigned long long)wt.seg);
+        atomicAdd(p.segments + 1, (unsigned long long)wt.sph);
+        atomicAdd(p.segments + 2, (unsigned long long)wt.box);
+    }
+}
+
 // ---- launchers (called from rt_host.cpp) ---------------------------------------------
 // cull: 0 = brute force (every sphere, index order), 7 = two-level cluster walk with
 // transposed member tests (the default)
@@ -1397,6 +1609,32 @@ hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t ld
     const void *fn = render_ptr(variant, cull, false);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
+}
+
+hipError_t launch_wave_gen(const KWave &w, hipStream_t stream)
+{
+    hipLaunchKernelGGL(wave_gen_kernel, dim3((w.n_chunk + 255u) / 256u), dim3(256), 0, stream, w);
+    return hipGetLastError();
+}
+
+static const void *wave_bounce_ptr(int cull, bool count)
+{
+    if (cull == 7) return count ? reinterpret_cast<const void *>(&wave_bounce_kernel<7, true>)
+                                : reinterpret_cast<const void *>(&wave_bounce_kernel<7, false>);
+    return count ? reinterpret_cast<const void *>(&wave_bounce_kernel<0, true>)
+                 : reinterpret_cast<const void *>(&wave_bounce_kernel<0, false>);
+}
+
+hipError_t launch_wave_bounce(int cull, const KWave &w, uint32_t grid, hipStream_t stream)
+{
+    const size_t lds = (size_t)w.p.lds_units * 16u;
+    void *args[] = {const_cast<KWave *>(&w)};
+    return hipLaunchKernel(wave_bounce_ptr(cull, w.p.segments != nullptr), dim3(grid), dim3(256), args, lds, stream);
+}
+
+hipError_t occupancy_wave_bounce(int cull, int *blocks_per_cu, size_t lds)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wave_bounce_ptr(cull, false), 256, lds);
 }
 
 hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream)

@@ -17,10 +17,11 @@ from .camera import Camera
 
 
 def make_params(width, height, spp, max_depth=64, seed=1234, row_offset=0, row_stride=1, num_rows=0,
-                full_frame=False, scalar_scene=False, fast_math=False, brute_force=False, cuda_compat=False):
+                full_frame=False, scalar_scene=False, fast_math=False, brute_force=False, cuda_compat=False,
+                wavefront=False):
     flags = (abi.RT_FLAG_FULL_FRAME if full_frame else 0) | (abi.RT_FLAG_SCALAR_SCENE if scalar_scene else 0) \
         | (abi.RT_FLAG_FAST_MATH if fast_math else 0) | (abi.RT_FLAG_BRUTE_FORCE if brute_force else 0) \
-        | (abi.RT_FLAG_CUDA_COMPAT if cuda_compat else 0)
+        | (abi.RT_FLAG_CUDA_COMPAT if cuda_compat else 0) | (abi.RT_FLAG_WAVEFRONT if wavefront else 0)
     return abi.RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, num_rows, flags)
 
 

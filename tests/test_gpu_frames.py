@@ -177,3 +177,41 @@ def test_alternating_caller_streams(pipeline, budget_samples, monkeypatch):
         _bits_equal(outs[k].cpu().numpy(), want, f"frame {k}")
         assert int(segs[k][0]) == want_seg
     ds.close()
+
+
+# ---- the wavefront variant (RT_FLAG_WAVEFRONT) -------------------------------
+@pytest.mark.parametrize("queue_rays", ["", "1000"])
+def test_wavefront_variant_matches_megakernel(queue_rays, monkeypatch):
+    """Per-segment launches through HBM ray queues (wave_gen_kernel, wave_bounce_kernel): the
+    same frames, bit for bit, and the same segment counts as the persistent megakernel, on the
+    huge scene (culled walk) and the simple scene (brute force, shading records in LDS), for
+    depth limits 0..64, both cameras, and chunks smaller than a pass (RT_WAVE_QUEUE_RAYS)."""
+    if queue_rays:
+        monkeypatch.setenv("RT_WAVE_QUEUE_RAYS", queue_rays)
+    for scene in ("huge", "simple"):
+        s, m = G.scene(scene)
+        for (W, H, spp, depth, mode) in [(64, 36, 4, 64, 0), (48, 27, 3, 64, 1), (40, 20, 5, 1, 0), (32, 16, 2, 0, 0),
+                                         (33, 17, 9, 3, 1)]:
+            cam = rt.Camera.default(W, H, mode)
+            a, sa = rt.render_f32((s, m), rt.make_params(W, H, spp, depth, 7), cam)
+            b, sb = rt.render_f32((s, m), rt.make_params(W, H, spp, depth, 7, wavefront=True), cam)
+            _bits_equal(b, a, f"{scene} {W}x{H} spp {spp} depth {depth} camera {mode}")
+            assert sb.segments == sa.segments and sb.primaries == sa.primaries
+
+
+def test_wavefront_variant_golden_and_multipass(monkeypatch):
+    """The wavefront variant against the reference's own frame (golden huge_64x36_s4) and a
+    multi-pass render (slot budget of 8 samples) against the oracle."""
+    meta, f32, _ = G.render("huge_64x36_s4")
+    s, m = G.scene("huge")
+    p = rt.make_params(meta["width"], meta["height"], meta["spp"], meta["depth"], meta["seed"], wavefront=True)
+    img, _ = rt.render_f32((s, m), p)
+    _bits_equal(img, f32, "golden huge_64x36_s4")
+    W, H, spp = 40, 24, 21
+    monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * 8))
+    monkeypatch.setenv("RT_WAVE_QUEUE_RAYS", "2000")
+    cam = O.camera_default(W, H)
+    img, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 3, wavefront=True), cam)
+    want, want_seg = O.render_f32(s, m, cam, rt.make_params(W, H, spp, 64, 3))
+    _bits_equal(img, want, "multi-pass")
+    assert st.segments == want_seg

@@ -205,7 +205,7 @@ int rt_scene_destroy(rt_scene *scene);
  * hardware queues - 1: 3 at HIP's default GPU_MAX_HW_QUEUES=4, at most 4) and 2 slot
  * workspaces per stream, so consecutive frames overlap; they read only the scene and the by-value
  * arguments, and the writes to d_rgb / d_segments are enqueued on `stream`, so results appear
- * in stream order (RT_PIPELINE=n in the environment sets the streams, 2..4; 0: all on
+ * in stream order (RT_PIPELINE=n in the environment sets the streams, 2..8; 0: all on
  * `stream`).                                                                                 */
 int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
                      float *d_rgb, void *stream, uint64_t *d_segments);

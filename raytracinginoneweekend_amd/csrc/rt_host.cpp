@@ -73,7 +73,7 @@ static_assert(kMaxSlotsBytes / 12 < (1ull << 32), "slot index width");
 // 2 x 8 queue lines, 2 x 4 u64 segment counters, then the compat kernel's pixel counter
 // internal render streams for frames in flight (RT_PIPELINE = 2..kMaxBufs), and workspaces:
 // RT_WS_PER_STREAM (1..2) per stream, at most kMaxWs
-constexpr uint32_t kMaxBufs = 4;
+constexpr uint32_t kMaxBufs = 8;
 constexpr uint32_t kMaxWs = 2 * kMaxBufs;
 // counters: [kMaxWs][8 queues x kQueueStride], then [kMaxWs][4] u64 segment counters, then
 // the compat kernel's counter
@@ -200,8 +200,8 @@ struct rt_scene {
     bool free_valid[kMaxWs] = {};
     // queue/segment counters of workspace b not known to be zero (set while a render using
     // them is enqueued, cleared once the accumulation that resets them is enqueued after it)
-    bool ctr_dirty[kMaxWs] = {true, true, true, true, true, true, true, true};
-    static_assert(kMaxWs == 8, "ctr_dirty initialiser lists one entry per workspace");
+    bool ctr_dirty[kMaxWs];
+    rt_scene() { std::fill(std::begin(ctr_dirty), std::end(ctr_dirty), true); }
     uint32_t next_buf = 0;  // workspace of the next render pass
     int last_ws = -1;       // workspace of the last render pass issued (its ev_done), -1 = none
     // the caller stream of the previous call and an event after the last work enqueued on it:
@@ -720,7 +720,9 @@ uint32_t pipeline_env()
     if (!e || !*e) {
         const char *q = std::getenv("GPU_MAX_HW_QUEUES");
         const unsigned long hw = q && *q ? std::strtoul(q, nullptr, 10) : 4ul;
-        return static_cast<uint32_t>(std::clamp<unsigned long>(hw > 1 ? hw - 1 : 1, 2, kMaxBufs));
+        // default at most 4: 4 / 6 / 7 streams measure alike on config 3 and its 8-way row share
+        // (profiles/r02/ab/pipeline_streams_*.txt), and each stream holds two slot workspaces
+        return static_cast<uint32_t>(std::clamp<unsigned long>(hw > 1 ? hw - 1 : 1, 2, 4));
     }
     const unsigned long v = std::strtoul(e, nullptr, 10);
     return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxBufs));

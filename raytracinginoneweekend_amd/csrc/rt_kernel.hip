@@ -68,7 +68,11 @@ __device__ __forceinline__ bool first_active_lane()
 enum DbgEvent : uint32_t {
     EV_ITER, EV_REFILL_TRIP, EV_FRESH, EV_REJECT_TRIP, EV_LENS_DONE, EV_SCATTER_DONE, EV_ROOT_GATE_PASS,
     EV_SUPER, EV_SUPER_PASS, EV_CLUSTER_REQ, EV_TRANSPOSED, EV_T_ROUND, EV_T_FAR, EV_PER_LANE_MEMBERS,
-    EV_SKY, EV_HIT, EV_LAMBERT, EV_UNIT_DIR, EV_DIELECTRIC, EV_STORE, EV_METAL_ABSORB, EV_COUNT
+    EV_SKY, EV_HIT, EV_LAMBERT, EV_UNIT_DIR, EV_DIELECTRIC, EV_STORE, EV_METAL_ABSORB,
+    EV_LIVE_LANES,  // live lanes summed over wave iterations
+    EV_DRY_ITER,    // wave iterations after the item queues ran dry (the drain)
+    EV_DRY_LANES,   // live lanes summed over those
+    EV_COUNT
 };
 static_assert(EV_COUNT <= kDbgEvents, "event counters");
 #define RT_EV(e)                                          \
@@ -912,6 +916,16 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         stamp(1);
         if (ballot(alive) == 0) break;  // only when the item space is exhausted
         RT_EV(EV_ITER);
+        if (STATS) {
+            const uint32_t nl = lanes(alive);
+            if (first_active_lane()) {
+                dbg.ev[EV_LIVE_LANES] += nl;
+                if (exhausted) {
+                    ++dbg.ev[EV_DRY_ITER];
+                    dbg.ev[EV_DRY_LANES] += nl;
+                }
+            }
+        }
         if (STATS && lane == 0) {
             ++dbg_iters;
             if (exhausted) {

@@ -21,7 +21,8 @@ a single-thread figure and the optimized CPU restatement beside it (BASELINE.md 
 
 roofline: executed sphere + box test FLOP per frame over the frame period (ms_per_step) against
 the f32 vector peak; traffic and VALU issue come from a rocprofv3 --pmc summary of the SAME
-build (profiles/pmc_render_c3.json, stamped with the library's sha256; dropped otherwise).
+build of the timed kernel (profiles/pmc_render_c3.json, stamped with the sha256 of that kernel's
+machine code and descriptor, kernel_sha256; dropped otherwise).
 """
 import argparse
 import json
@@ -105,9 +106,63 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
+TIMED_KERNEL = "_ZN2rt13render_kernelILi0ELi7ELb0ELb0EEEvNS_7KParamsE"  # rt::render_kernel<0, 7, false, false>
+
+
+def _elf_sections(b):
+    import struct
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    hdrs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    stro = hdrs[shstrndx][4]
+    return {b[stro + h[0]:b.index(b"\0", stro + h[0])].decode(): h for h in hdrs}, hdrs
+
+
+def kernel_sha256(symbol=TIMED_KERNEL):
+    """sha256 of one kernel's machine code and kernel descriptor in the gfx950 code objects of
+    the loaded library (PMC summaries are stamped with it, so host-side or other-instantiation
+    changes do not invalidate them); None if the symbol is not found."""
+    import hashlib
+    import struct
+    from raytracinginoneweekend_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        so = f.read()
+    secs, _ = _elf_sections(so)
+    h = secs[".hip_fatbin"]
+    fat = so[h[4]:h[4] + h[5]]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    digest, pos = hashlib.sha256(), fat.find(magic)
+    found = False
+    while pos >= 0:
+        n, = struct.unpack_from("<Q", fat, pos + 24)
+        q = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", fat, q)
+            triple = fat[q + 24:q + 24 + tlen].decode()
+            q += 24 + tlen
+            if "gfx950" not in triple:
+                continue
+            co = fat[pos + off:pos + off + size]
+            cs, hdrs = _elf_sections(co)
+            if ".symtab" not in cs:
+                continue
+            sym, stra = cs[".symtab"], cs[".strtab"][4]
+            for i in range(sym[5] // 24):
+                name_off, info, other, shndx, value, ssize = struct.unpack_from("<IBBHQQ", co, sym[4] + 24 * i)
+                name = co[stra + name_off:co.index(b"\0", stra + name_off)].decode()
+                if name in (symbol, symbol + ".kd") and ssize:
+                    sh = hdrs[shndx]
+                    start = sh[4] + value - sh[3]
+                    digest.update(name.encode() + co[start:start + ssize])
+                    found = True
+        pos = fat.find(magic, pos + 1)
+    return digest.hexdigest() if found else None
+
+
 def pmc_fields(path, kernel, config):
     """HBM traffic and VALU issue of the render kernel from a committed rocprofv3 --pmc summary
-    (scripts/pmc_json.py) of the same kernel, workload AND build (sha256 of librt_mi355x.so);
+    (scripts/pmc_json.py) of the same kernel, workload AND build (sha256 of the timed kernel's
+    machine code and descriptor, kernel_sha256);
     (record, status) with record None when absent, mismatched or from another build."""
     try:
         with open(path) as f:
@@ -116,9 +171,9 @@ def pmc_fields(path, kernel, config):
         return None, "absent"
     if rec.get("kernel") != kernel or rec.get("config") != config:
         return None, "other kernel or workload"
-    if rec.get("lib_sha256") != lib_sha256():
-        return None, "stale: summary of another build of librt_mi355x.so"
-    return rec, "current build"
+    if rec.get("kernel_sha256") != kernel_sha256():
+        return None, "stale: summary of another build of the timed kernel"
+    return rec, "current build of the timed kernel"
 
 
 def frames_in_flight():

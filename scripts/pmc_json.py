@@ -52,13 +52,14 @@ need = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]
 missing = [c for c in need if c not in m]
 if missing:
     raise SystemExit(f"missing counters {missing} for kernel {a.kernel!r} under {a.root}")
-from bench import WORKLOAD, lib_sha256  # noqa: E402
+from bench import WORKLOAD, kernel_sha256, lib_sha256  # noqa: E402
 
 t = sum(dur) / len(dur)
 cycles = m["GRBM_GUI_ACTIVE"] / 8.0
 rec = {
     "kernel": a.kernel,
     # the build these counters describe: bench.py uses them only for the same library
+    "kernel_sha256": kernel_sha256(),
     "lib_sha256": lib_sha256(),
     "config": {"workload": WORKLOAD[a.config], "camera": a.camera, "traversal": a.traversal, "n_gpus": 1},
     "dispatch_ms": round(t * 1e3, 4),

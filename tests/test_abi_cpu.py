@@ -178,3 +178,12 @@ def test_cuda_variant_oracle_engine_and_pixel_zero():
     img, seg = O.render_cuda_compat(s, m, rt.Camera.cuda(W, H).c, p)
     assert np.isfinite(img).all() and seg >= W * H * 4
     assert (img[0, 0] > 0).all()  # sky colour
+
+
+def test_timed_kernel_code_hash():
+    """bench.py stamps PMC summaries with the sha256 of the timed kernel's machine code and
+    descriptor (rt::render_kernel<0, 7, false, false>), found in the library's gfx950 code object."""
+    import bench
+    h = bench.kernel_sha256()
+    assert h is not None and len(h) == 64
+    assert bench.kernel_sha256("no_such_kernel") is None

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Round profiles of the current build: bench line (with the CPU baseline), rocprofv3 kernel
-# stats of the same command, PMC passes -> pmc_render.json (stamped with the library's sha256),
+# stats of the same command, PMC passes -> pmc_render.json (stamped with the timed kernel's code hash),
 # then the bench line again reading that summary. Output under gpurun_out/$TAG/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

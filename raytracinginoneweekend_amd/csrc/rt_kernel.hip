@@ -658,18 +658,6 @@ __device__ __forceinline__ float4 gld4(const float4 *p, uint32_t i)
 // Structure 7 (the default) is held to 6 waves per SIMD: unhinted it takes 83 VGPRs (5 waves);
 // hinted, the allocator keeps 79 and parks one 12-byte constant that only the metal-absorption
 // path reloads (measured: 5.03-5.06 ms vs 5.19-5.24 per config-3 launch).
-// A wave that finds every item queue dry only drains its live paths (the deep ones, up to
-// max_depth iterations): it takes a higher issue priority than the waves still dealing items
-// (other launches' bulk work under frames in flight), so the launch ends, and its workgroup
-// slots free, sooner. Same instructions, same bits.
-#ifndef RT_DRAIN_PRIO
-#define RT_DRAIN_PRIO 0
-#endif
-__device__ __forceinline__ void drain_priority()
-{
-    if (RT_DRAIN_PRIO > 0) __builtin_amdgcn_s_setprio(RT_DRAIN_PRIO);
-}
-
 template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? 6 : RT_MIN_WAVES_PER_SIMD;
 template <int V, int CULL, bool STATS, bool COUNT>
@@ -794,10 +782,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     const uint32_t s0 = S(c);
                     if (s0 >= B) {
                         q = (q + 1u) & 7u;
-                        if (++q_tried == 8u) {
-                            exhausted = true;
-                            drain_priority();
-                        }
+                        if (++q_tried == 8u) exhausted = true;
                         continue;
                     }
                     cnext = 64u * (qb0 + s0);
@@ -806,10 +791,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                 const uint64_t chunk = (uint64_t)q + 8ull * c;
                 if (chunk >= p.n_chunks) {
                     q = (q + 1u) & 7u;
-                    if (++q_tried == 8u) {
-                        exhausted = true;
-                        drain_priority();
-                    }
+                    if (++q_tried == 8u) exhausted = true;
                     continue;
                 }
                 // big chunks first, then 64-item chunks for the end of the launch: a wave

@@ -40,6 +40,20 @@ struct FrameConsts {
     uint32_t div_fast;  // bit 0 / 1: x / width, x / height by rW / rH + one FMA correction is exact
 };
 
+// The deep queue of one workspace (structure of arrays, 8 regions of rcap paths): f =
+// [9][8 rcap] floats {o.xyz, d.xyz, attenuation.xyz} of the next segment, the data-stream state
+// and the sample's slot index. Region r is appended to by workgroups r mod 8; its counters sit in
+// the workspace's queue-counter block, line r: word kDeepCount = paths appended (may exceed
+// rcap: lanes past it keep their path), word kDeepDeal = the deep launch's dealing counter;
+// they are reset with the queue counters.
+struct DeepQueue {
+    float *f;
+    uint64_t *rng;
+    uint32_t *slot;
+    uint32_t *ctr;           // the workspace's queue-counter block (8 x kQueueStride words)
+    uint32_t rcap;
+};
+
 struct KParams {
     FrameConsts fc;
     // camera basis (rt_camera)
@@ -83,6 +97,12 @@ struct KParams {
     uint32_t *queue_ctr;     // [8 x kQueueStride]: one counter per 256-B line
     unsigned long long *segments;  // optional [3]: segments, sphere tests, cluster box tests
     unsigned long long *dbg;       // [kDbgWords] diagnostics (V_STATS_LDS only)
+    // deep-path split: a path that has traced deep_depth segments leaves the
+    // launch through the deep queue (whole state, stream order unchanged) and a second launch
+    // of the same kernel (deep_mode = the split depth) deals the queued paths densely over its lanes.
+    DeepQueue deep;
+    uint32_t deep_depth;     // 0: no split (and always 0 in the deep launch)
+    uint32_t deep_mode;      // the deep launch: the split depth (its paths resume there); 0 otherwise
 };
 
 struct KAccum {
@@ -135,6 +155,8 @@ struct KWave {
 
 // queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise
 constexpr uint32_t kQueueStride = 64;
+constexpr uint32_t kDeepDeal = 16;   // word of queue q's line (the deep launch deals while the queue counter is idle)
+constexpr uint32_t kDeepCount = 32;  // word of queue q's line, in its second 128-B half
 
 // V_STATS_LDS diagnostics buffer: 16 counters, then {start, exit, iterations, hw id | refills}
 // per wave

@@ -75,6 +75,7 @@ static_assert(kMaxSlotsBytes / 12 < (1ull << 32), "slot index width");
 // RT_WS_PER_STREAM (1..2) per stream, at most kMaxWs
 constexpr uint32_t kMaxBufs = 8;
 constexpr uint32_t kMaxWs = 2 * kMaxBufs;
+constexpr uint32_t kDeepSplitDefault = 8;  // RT_DEEP_SPLIT
 // counters: [kMaxWs][8 queues x kQueueStride], then [kMaxWs][4] u64 segment counters, then
 // the compat kernel's counter
 constexpr size_t kSegWords = kMaxWs * 8 * rt::kQueueStride;
@@ -191,6 +192,8 @@ struct rt_scene {
     size_t slots_bytes[kMaxWs] = {};
     float *acc = nullptr;
     size_t acc_bytes = 0;
+    void *deep[kMaxWs] = {};  // deep-path split: the deep queue of each workspace (rt::DeepQueue)
+    size_t deep_bytes[kMaxWs] = {};
     void *wq = nullptr;  // RT_FLAG_WAVEFRONT: two ray queues and their counters
     size_t wq_bytes = 0;
     int occ_wave[2] = {-1, -1};  // wave_bounce_kernel blocks per CU [culled], -1 = unknown
@@ -694,7 +697,29 @@ uint32_t root_box_env()
     return e && e[0] == '0' ? 0u : 1u;
 }
 
-
+// Deep-path split (render_kernel): paths that have traced RT_DEEP_SPLIT segments continue in a
+// second launch of the same kernel that deals them densely (0 = no split). Same bits either way.
+uint32_t deep_split_env()
+{
+    const char *e = std::getenv("RT_DEEP_SPLIT");
+    return e && *e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : kDeepSplitDefault;
+}
+// deep queue of a pass: 8 regions of 1/1024 of its samples each (at least 512): 0.8% of the
+// samples, where 0.2-0.3% reach the split depth on config 3; paths past a full region stay in the
+// main launch. Passes of fewer than RT_DEEP_MIN_ITEMS samples (default 2^26) are not split: the
+// deep launch is a serial tail of about max_depth - split iterations, which a small pass's own
+// drain does not outweigh (config 3's 8-way row share: 0.58-0.65 vs 0.52 ms per frame).
+uint32_t deep_region_cap(uint32_t n_items)
+{
+    const char *e = std::getenv("RT_DEEP_REGION_DIV");
+    const unsigned long div = e && *e ? std::max(1ul, std::strtoul(e, nullptr, 10)) : 1024ul;
+    return std::max<uint32_t>(512u, static_cast<uint32_t>(n_items / div));
+}
+uint64_t deep_min_items_env()
+{
+    const char *e = std::getenv("RT_DEEP_MIN_ITEMS");
+    return e && *e ? std::strtoull(e, nullptr, 10) : (1ull << 26);
+}
 
 } // namespace
 
@@ -824,6 +849,8 @@ int rt_scene_destroy(rt_scene *sc)
     for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr, sc->wq})
         if (p) (void)hipFree(p);
     for (float *p : sc->slots)
+        if (p) (void)hipFree(p);
+    for (void *p : sc->deep)
         if (p) (void)hipFree(p);
     (void)hipSetDevice(prev);
     delete sc;
@@ -1096,6 +1123,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // work that last read workspace w (the accumulation of pass p - n_ws); render kernels
     // touch no caller memory, so the caller stream sees the same results in the same order.
     // RT_PIPELINE=0: everything on the caller stream.
+    const uint32_t deep_split = deep_split_env();
+    const uint64_t deep_min_items = deep_min_items_env();
     const uint32_t bufs = wave ? 1u : pipeline_env();  // the wavefront variant: caller stream only
     const bool pipe = bufs > 1;
     const uint32_t n_ws = pipe ? bufs * ws_per_stream_env() : 1u;
@@ -1169,6 +1198,20 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u);
+        // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
+        k.deep_depth = 0;
+        k.deep_mode = 0;
+        if (deep_split && !wave && deep_split < P.max_depth && k.n_items >= deep_min_items) {
+            const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
+            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], static_cast<size_t>(cap) * 48u); rc) return rc;
+            char *base = static_cast<char *>(sc->deep[wb]);
+            k.deep.f = reinterpret_cast<float *>(base);
+            k.deep.rng = reinterpret_cast<uint64_t *>(base + static_cast<size_t>(cap) * 36u);
+            k.deep.slot = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 44u);
+            k.deep.ctr = k.queue_ctr;
+            k.deep.rcap = rcap;
+            k.deep_depth = deep_split;
+        }
         if (verbose())
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) %s%u\n",
                          variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1,
@@ -1196,6 +1239,12 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             }
         } else {
             RT_HIP(rt::launch_render(variant, cull_mode, k, grid, xst));
+            if (k.deep_depth) {  // the deep launch: the queued paths, same grid, same stream
+                rt::KParams kd = k;
+                kd.deep_mode = k.deep_depth;
+                kd.deep_depth = 0;
+                RT_HIP(rt::launch_render(variant, cull_mode, kd, grid, xst));
+            }
         }
         if (variant == rt::V_STATS_LDS) sc->dbg_waves = grid * 4u;
         if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], xst));

@@ -696,10 +696,11 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     }
     __shared__ float4 lds_pn[256];  // per lane: a pending metal scatter's normal and roughness
 
-    // wave-uniform cursor over the item space
+    // wave-uniform cursor over the item space (the deep launch: over the queued paths)
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
     uint32_t cnext = 0, cend = 0;
     bool exhausted = false;
+    bool deep_full = false;  // this wave's deep-queue region is full: no more splits
 
     // lane state: the lane's item is one sample (pixel enumeration index, sample of the pass)
     bool alive = false;
@@ -762,6 +763,20 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             RT_EV(EV_REFILL_TRIP);
             if (cnext >= cend) {
                 uint32_t c = 0;
+                if (p.deep_mode) {
+                    // the deep launch: 64 queued paths per grab from region q, then the next
+                    // region (a wave starts on its workgroup's region)
+                    if (lane == 0) c = atomicAdd(p.deep.ctr + q * kQueueStride + kDeepDeal, 1u);
+                    c = __builtin_amdgcn_readfirstlane(c);
+                    const uint32_t nq = min(p.deep.ctr[q * kQueueStride + kDeepCount], p.deep.rcap);
+                    if (c >= (nq + 63u) / 64u) {
+                        q = (q + 1u) & 7u;
+                        if (++q_tried == 8u) exhausted = true;
+                        continue;
+                    }
+                    cnext = q * p.deep.rcap + 64u * c;
+                    cend = q * p.deep.rcap + min(64u * c + 64u, nq);
+                } else {
                 if (lane == 0) c = atomicAdd(p.queue_ctr + q * kQueueStride, 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
                 if (p.guided_l2b < 0.f) {
@@ -804,15 +819,32 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     cend = min(cnext + 64u, p.n_items);
                 }
                 }
+                }
             }
             const uint32_t avail = cend - cnext;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (!alive && rank < avail) {
                 const uint32_t I = cnext + rank;
-                ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
-                pix = I - ls * fc->n_pixels;
-                alive = fresh = true;
+                if (p.deep_mode) {
+                    // a queued path resumes where the main launch left it: the ray of its next
+                    // segment, attenuation, data stream and segment count; ls = 0 and pix = the
+                    // slot index address the same slot
+                    const uint32_t cap = 8u * p.deep.rcap;
+                    const float *f = p.deep.f;
+                    o = mk(f[I], f[cap + I], f[2 * cap + I]);
+                    d = mk(f[3 * cap + I], f[4 * cap + I], f[5 * cap + I]);
+                    att = mk(f[6 * cap + I], f[7 * cap + I], f[8 * cap + I]);
+                    rng = p.deep.rng[I];
+                    pix = p.deep.slot[I];
+                    ls = 0;
+                    depth = p.deep_mode;
+                    alive = true;
+                } else {
+                    ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
+                    pix = I - ls * fc->n_pixels;
+                    alive = fresh = true;
+                }
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
             cnext += took;
@@ -915,6 +947,40 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         }
         stamp(1);
         if (ballot(alive) == 0) break;  // only when the item space is exhausted
+        // ---- deep-path split: a path that has traced deep_depth segments (with its scatter
+        // resolved) moves to the deep queue, whole state, and the lane takes a new item next
+        // iteration. The few paths that run to max_depth (the reference's refract traps rays in
+        // glass spheres) then no longer hold this launch's waves for ~max_depth iterations after
+        // the item queues run dry; the deep launch runs them with every lane busy. Each path
+        // sees the same operations and draws in the same order: same bits.
+        // Paths are appended to region blockIdx % 8 of the queue (8 counters on separate
+        // lines, so the appends of the whole grid do not serialise on one address); a wave
+        // that finds its region full stops splitting.
+        if (p.deep_depth && !deep_full) {
+            const bool dv = alive && !defer && depth == p.deep_depth;
+            const uint64_t m = ballot(dv);
+            if (m) {
+                const uint32_t r = blockIdx.x & 7u;
+                const uint32_t nm = (uint32_t)__popcll(m);
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(p.deep.ctr + r * kQueueStride + kDeepCount, nm);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (base + nm >= p.deep.rcap) deep_full = true;
+                uint32_t j = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (dv && j < p.deep.rcap) {
+                    const uint32_t cap = 8u * p.deep.rcap;
+                    j += r * p.deep.rcap;
+                    float *f = p.deep.f;
+                    f[j] = o.x; f[cap + j] = o.y; f[2 * cap + j] = o.z;
+                    f[3 * cap + j] = d.x; f[4 * cap + j] = d.y; f[5 * cap + j] = d.z;
+                    f[6 * cap + j] = att.x; f[7 * cap + j] = att.y; f[8 * cap + j] = att.z;
+                    p.deep.rng[j] = rng;
+                    p.deep.slot[j] = ls * fc->n_pixels + pix;
+                    alive = false;
+                }
+            }
+        }
         RT_EV(EV_ITER);
         if (STATS) {
             const uint32_t nl = lanes(alive);

@@ -215,3 +215,49 @@ def test_wavefront_variant_golden_and_multipass(monkeypatch):
     want, want_seg = O.render_f32(s, m, cam, rt.make_params(W, H, spp, 64, 3))
     _bits_equal(img, want, "multi-pass")
     assert st.segments == want_seg
+
+
+# ---- the deep-path split (RT_DEEP_SPLIT, render_kernel deep queue) --------------------------
+@pytest.mark.parametrize("split", ["1", "3", "8"])
+def test_deep_split_matches_unsplit(split, monkeypatch):
+    """Paths that have traced RT_DEEP_SPLIT segments move to the deep queue and finish in a second
+    launch: the same frames, bit for bit, and the same segment counts as without the split
+    (RT_DEEP_SPLIT=0), for both cameras, depth limits around the split, multi-pass frames (slot
+    budget of 8 samples) and a deep queue that overflows (split 1 on 230 K samples with the
+    corrected camera: 8 regions of 512 paths, most paths continue past their first segment),
+    whose extra paths stay in the main launch. Configs 4 and 5 (test_full_config_frame_...) run
+    with the default split, their passes being above RT_DEEP_MIN_ITEMS."""
+    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")  # split passes of any size
+    s, m = G.scene("huge")
+    cases = [(64, 36, 4, 64, 0, 0), (48, 27, 3, 64, 1, 0), (40, 20, 5, int(split), 0, 0),
+             (33, 17, 9, int(split) + 1, 1, 0), (40, 24, 21, 64, 0, 8), (160, 90, 16, 64, 1, 0)]
+    for (W, H, spp, depth, mode, budget) in cases:
+        cam = rt.Camera.default(W, H, mode)
+        if budget:
+            monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget))
+        monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+        a, sa = rt.render_f32((s, m), rt.make_params(W, H, spp, depth, 11), cam)
+        monkeypatch.setenv("RT_DEEP_SPLIT", split)
+        b, sb = rt.render_f32((s, m), rt.make_params(W, H, spp, depth, 11), cam)
+        monkeypatch.delenv("RT_SLOT_BUDGET_BYTES", raising=False)
+        _bits_equal(b, a, f"split {split}: {W}x{H} spp {spp} depth {depth} camera {mode}")
+        assert sb.segments == sa.segments and sb.primaries == sa.primaries
+
+
+def test_deep_split_against_oracle_and_golden(monkeypatch):
+    """With the split at 2 segments (most continuing paths go through the deep queue): the
+    reference's own frame (golden huge_64x36_s4) and the oracle on a multi-pass render."""
+    monkeypatch.setenv("RT_DEEP_SPLIT", "2")
+    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
+    meta, f32, _ = G.render("huge_64x36_s4")
+    s, m = G.scene("huge")
+    img, _ = rt.render_f32((s, m), rt.make_params(meta["width"], meta["height"], meta["spp"], meta["depth"],
+                                                  meta["seed"]))
+    _bits_equal(img, f32, "golden huge_64x36_s4")
+    W, H, spp = 40, 24, 21
+    monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * 8))
+    cam = O.camera_default(W, H, abi.RT_CAMERA_CORRECTED)
+    img, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 5), rt.Camera.default(W, H, rt.CORRECTED))
+    want, want_seg = O.render_f32(s, m, cam, rt.make_params(W, H, spp, 64, 5))
+    _bits_equal(img, want, "multi-pass, corrected camera")
+    assert st.segments == want_seg

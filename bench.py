@@ -418,7 +418,11 @@ def main():
                        + f", {args.traversal}", "parallelism": f"row-interleaved x{world}, RCCL gather of "
                        + ("u8 (gamma epilogue per rank)" if rgb8 else "f32") + " tiles",
                        "output": args.output, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                       "hw_queues_env": hw_env},
+                       "hw_queues_env": hw_env,
+                       # deep-path split: split depth, and the pass size below which
+                       # passes are not split (library defaults unless set in the environment)
+                       "deep_split": int(os.environ.get("RT_DEEP_SPLIT", "8")),
+                       "deep_min_items": int(os.environ.get("RT_DEEP_MIN_ITEMS", str(1 << 26)))},
             # ms_per_step is the steady-state period of a frame stream (frames in flight);
             # frame_wall_ms is ONE frame alone, start to finish (render, accumulate, gather)
             "frame_wall_ms": r3(main_m["frame_latency_ms"]),
@@ -456,7 +460,7 @@ def main():
         if pmc and not rehearse:
             # HBM bytes per frame (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, one
             # launch per frame here) and the VALU issue, from the PMC summary of THIS build
-            rec["roofline"]["traffic"] = pmc["hbm_bytes_per_launch"]
+            rec["roofline"]["traffic"] = pmc["hbm_bytes_per_frame"]
             rec["roofline"]["traffic_unit"] = "bytes/frame"
             rec["roofline"]["valu_insts_per_frame"] = pmc["valu_insts"]
             # VALU pipe busy over the frame period: wave64 VALU = 2 cycles, 1024 SIMDs

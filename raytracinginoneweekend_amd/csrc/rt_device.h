@@ -121,6 +121,12 @@ struct KAccum {
     // the render's queue counters, zeroed here for the next render on this workspace
     uint32_t *queue_reset;
     uint32_t queue_words;
+    // deep-path split: a region appended past deep_rcap (paths left in the main launch) makes
+    // the thread that resets its counter write deep_key (the render's camera key) to *deep_over,
+    // host memory the library reads on later calls (no split for that camera on this scene)
+    unsigned long long *deep_over;
+    unsigned long long deep_key;
+    uint32_t deep_rcap;
 };
 
 // RT_FLAG_CUDA_COMPAT: the semantics of the reference's CUDA variant (src/CUDA/cuda_impl.cu),

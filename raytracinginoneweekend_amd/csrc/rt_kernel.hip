@@ -1381,7 +1381,11 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
     // the render that used this workspace has finished: reset its queue counters (no memset
     // kernel in front of the next render)
     if (k.queue_reset)
-        for (uint32_t w = i; w < k.queue_words; w += gridDim.x * blockDim.x) k.queue_reset[w] = 0u;
+        for (uint32_t w = i; w < k.queue_words; w += gridDim.x * blockDim.x) {
+            if (k.deep_over && (w & (kQueueStride - 1u)) == kDeepCount && k.queue_reset[w] > k.deep_rcap)
+                *k.deep_over = k.deep_key;
+            k.queue_reset[w] = 0u;
+        }
     if (i >= k.n_pixels) return;
     f3 acc;
     if (k.first) acc = mk(0.f, 0.f, 0.f);

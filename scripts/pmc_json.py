@@ -4,8 +4,8 @@
     python scripts/pmc_json.py <pmc dir with p*/run_counter_collection.csv> <out.json> \
         [--kernel 'render_kernel<0, 7, false, false>'] [--config c3] [--camera reference]
 
-Per dispatch of the kernel (mean over dispatches and passes):
-  hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE counts half of the
+Per frame (the kernel's dispatches of a frame summed, mean over frames and passes):
+  hbm_bytes_per_frame  = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE counts half of the
                          bytes of wide streaming reads on gfx950, MI355X_MICROARCH.md HBM section)
   valu_busy            = SQ_INSTS_VALU x 2 cycles / (SIMDs x GRBM_GUI_ACTIVE / 8)
                          (wave64 VALU issue = 2 cycles; GRBM_GUI_ACTIVE sums the 8 XCDs)
@@ -28,25 +28,29 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")
 ap.add_argument("--traversal", default="cull")
 ap.add_argument("--simds", type=int, default=1024)  # 256 CUs x 4 SIMDs
+ap.add_argument("--dispatches-per-frame", type=int, default=2)
 a = ap.parse_args()
 
+# Per frame: every dispatch of the kernel in a pass summed and divided by the frames, i.e. the
+# dispatches / --dispatches-per-frame (2 with the deep-path split on a one-pass frame such as
+# config 3: the main launch and the deep launch; 1 without it).
 vals = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_counter_collection.csv"))):
     per = defaultdict(float)
+    disp = set()
     for r in csv.DictReader(open(f)):
         if a.kernel not in r["Kernel_Name"]:
             continue
-        per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-    by = defaultdict(list)
-    for (_, c), v in per.items():
-        by[c].append(v)
-    for c, v in by.items():
-        vals[c].append(sum(v) / len(v))
+        disp.add(r["Dispatch_Id"])
+        per[r["Counter_Name"]] += float(r["Counter_Value"])
+    for c, v in per.items():
+        vals[c].append(v * a.dispatches_per_frame / len(disp))
 dur = []
 for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_kernel_trace.csv"))):
-    for r in csv.DictReader(open(f)):
-        if a.kernel in r["Kernel_Name"]:
-            dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+          for r in csv.DictReader(open(f)) if a.kernel in r["Kernel_Name"]]
+    if ds:
+        dur.append(sum(ds) * a.dispatches_per_frame / len(ds))
 m = {c: sum(v) / len(v) for c, v in vals.items()}
 need = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]
 missing = [c for c in need if c not in m]
@@ -62,9 +66,12 @@ rec = {
     "kernel_sha256": kernel_sha256(),
     "lib_sha256": lib_sha256(),
     "config": {"workload": WORKLOAD[a.config], "camera": a.camera, "traversal": a.traversal, "n_gpus": 1},
-    "dispatch_ms": round(t * 1e3, 4),
+    # per frame: the kernel's dispatches of one frame (durations summed: a span of overlapping
+    # launches when frames are in flight)
+    "kernel_ms_per_frame": round(t * 1e3, 4),
+    "dispatches_per_frame": a.dispatches_per_frame,
     "clock_ghz": round(cycles / t / 1e9, 3),
-    "hbm_bytes_per_launch": int(2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024),
+    "hbm_bytes_per_frame": int(2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024),
     "fetch_bytes_corrected": int(2 * m["FETCH_SIZE"] * 1024),
     "write_bytes": int(m["WRITE_SIZE"] * 1024),
     "valu_insts": m["SQ_INSTS_VALU"],

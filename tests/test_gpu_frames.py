@@ -261,3 +261,37 @@ def test_deep_split_against_oracle_and_golden(monkeypatch):
     want, want_seg = O.render_f32(s, m, cam, rt.make_params(W, H, spp, 64, 5))
     _bits_equal(img, want, "multi-pass, corrected camera")
     assert st.segments == want_seg
+
+
+def test_deep_split_overflow_feedback(monkeypatch):
+    """One scene, frames with two cameras streamed without host sync, split at 1 segment on every
+    pass: the corrected camera's passes overflow the deep queue, report it through host memory,
+    and its later frames run unsplit, while the reference camera's frames keep the split. Every
+    frame equals the unsplit render, bit for bit, with the same segment count."""
+    torch = pytest.importorskip("torch")
+    import time
+    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
+    monkeypatch.setenv("RT_DEEP_SPLIT", "1")
+    W, H, spp = 160, 90, 16
+    s, m = G.scene("huge")
+    cams = [rt.Camera.default(W, H, rt.CORRECTED), rt.Camera.default(W, H)]
+    ds = rt.DeviceScene((s, m))
+    p = rt.make_params(W, H, spp, 64, 21)
+    st = torch.cuda.current_stream()
+    outs, segs = [], []
+    for k in range(8):
+        outs.append(torch.empty((H, W, 3), dtype=torch.float32, device="cuda"))
+        segs.append(torch.zeros(3, dtype=torch.int64, device="cuda"))
+        ds.render(cams[k % 2].c, p, outs[-1].data_ptr(), st.cuda_stream, segs[-1].data_ptr())
+        if k == 3:
+            torch.cuda.synchronize()
+            time.sleep(0.01)
+    torch.cuda.synchronize()
+    ds.close()
+    monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+    for c, cam in enumerate(cams):
+        want, want_st = rt.render_f32((s, m), p, cam)
+        for k in range(c, 8, 2):
+            _bits_equal(outs[k].cpu().numpy(), want, f"frame {k} camera {c}")
+            assert int(segs[k][0]) == want_st.segments
+

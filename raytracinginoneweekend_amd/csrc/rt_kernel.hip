@@ -946,7 +946,12 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             }
         }
         stamp(1);
-        if (ballot(alive) == 0) break;  // only when the item space is exhausted
+        // no live lane: the item space is exhausted, or every lane's metal path was absorbed
+        // above (the refill then continues with the wave's chunk)
+        if (ballot(alive) == 0) {
+            if (exhausted) break;
+            continue;
+        }
         // ---- deep-path split: a path that has traced deep_depth segments (with its scatter
         // resolved) moves to the deep queue, whole state, and the lane takes a new item next
         // iteration. The few paths that run to max_depth (the reference's refract traps rays in

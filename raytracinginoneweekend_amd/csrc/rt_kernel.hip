@@ -756,12 +756,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         fc_ptr_t fc = fc_base;
         asm volatile("" : "+s"(fc));
         // ---- refill items for idle lanes and start their samples -------------------
-#ifdef RT_DEEP_LANES  // A/B: the deep launch keeps at most this many lanes of a wave busy
-        const bool lane_ok = !p.deep_mode || lane < RT_DEEP_LANES;
-#else
-        const bool lane_ok = true;
-#endif
-        uint64_t need = ballot(!alive && lane_ok);
+        uint64_t need = ballot(!alive);
         bool fresh = false;
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
@@ -853,7 +848,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
             cnext += took;
-            need = ballot(!alive && lane_ok);
+            need = ballot(!alive);
         }
 
         stamp(0);

@@ -295,3 +295,25 @@ def test_deep_split_overflow_feedback(monkeypatch):
             _bits_equal(outs[k].cpu().numpy(), want, f"frame {k} camera {c}")
             assert int(segs[k][0]) == want_st.segments
 
+
+
+@pytest.mark.parametrize("pipeline", ["", "0"])
+def test_deep_split_variants_and_row_shares(pipeline, monkeypatch):
+    """The split with every render variant it applies to (fast-math, brute force, the scalar-cache
+    scene, the simple scene's brute-force walk), on the caller's stream alone (RT_PIPELINE=0) or
+    on the render streams, and for interleaved row shares: each equals its unsplit render."""
+    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
+    monkeypatch.setenv("RT_PIPELINE", pipeline)
+    W, H, spp = 72, 40, 8
+    for scene, kw, rows in [("huge", dict(fast_math=True), {}), ("huge", dict(brute_force=True), {}),
+                            ("huge", dict(scalar_scene=True), {}), ("simple", {}, {}),
+                            ("huge", {}, dict(row_offset=2, row_stride=3, num_rows=13))]:
+        s, m = G.scene(scene)
+        cam = rt.Camera.default(W, H)
+        p = rt.make_params(W, H, spp, 64, 9, **rows, **kw)
+        monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+        a, sa = rt.render_f32((s, m), p, cam)
+        monkeypatch.setenv("RT_DEEP_SPLIT", "2")
+        b, sb = rt.render_f32((s, m), p, cam)
+        _bits_equal(b, a, f"{scene} {kw} {rows}")
+        assert sb.segments == sa.segments

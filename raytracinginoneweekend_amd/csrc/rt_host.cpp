@@ -719,6 +719,12 @@ uint32_t deep_region_cap(uint32_t n_items)
     const unsigned long div = e && *e ? std::max(1ul, std::strtoul(e, nullptr, 10)) : 1024ul;
     return std::max<uint32_t>(512u, static_cast<uint32_t>(n_items / div));
 }
+// RT_DEEP_ROOT_BOX=1 keeps the level-3 box gate in the deep launch (A/B; default off)
+bool deep_root_box_env()
+{
+    const char *e = std::getenv("RT_DEEP_ROOT_BOX");
+    return e && e[0] == '1';
+}
 // a nonzero key of the camera basis and the depth limit (FNV-1a over their bytes)
 unsigned long long camera_key(const rt_camera &c, uint32_t max_depth)
 {
@@ -1276,6 +1282,9 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 rt::KParams kd = k;
                 kd.deep_mode = k.deep_depth;
                 kd.deep_depth = 0;
+                // the deep paths bounce inside glass spheres, inside the box over all clusters:
+                // the level-3 gate only costs there (3.18-3.19 vs 3.22-3.24 ms/frame, same bits)
+                kd.use_root = deep_root_box_env() ? k.use_root : 0u;
                 RT_HIP(rt::launch_render(variant, cull_mode, kd, grid, xst));
             }
         }

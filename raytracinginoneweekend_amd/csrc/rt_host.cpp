@@ -1283,7 +1283,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 kd.deep_mode = k.deep_depth;
                 kd.deep_depth = 0;
                 // the deep paths bounce inside glass spheres, inside the box over all clusters:
-                // the level-3 gate only costs there (3.18-3.19 vs 3.22-3.24 ms/frame, same bits)
+                // the level-3 gate only costs there (alike within box noise, fewer box tests;
+                // same bits)
                 kd.use_root = deep_root_box_env() ? k.use_root : 0u;
                 RT_HIP(rt::launch_render(variant, cull_mode, kd, grid, xst));
             }

@@ -52,6 +52,8 @@ struct DeepQueue {
     uint32_t *slot;
     uint32_t *ctr;           // the workspace's queue-counter block (8 x kQueueStride words)
     uint32_t rcap;
+    uint8_t *px;             // [n_pixels] 1: some sample of the pixel went to the queue (cleared by
+                             // the accumulation that reads it)
 };
 
 struct KParams {
@@ -127,6 +129,12 @@ struct KAccum {
     unsigned long long *deep_over;
     unsigned long long deep_key;
     uint32_t deep_rcap;
+    // split passes accumulate in two parts: part 1 (after the main launch, beside the deep one)
+    // the pixels none of whose samples went to the deep queue, part 2 (after the deep launch)
+    // the others, clearing their flags; part 3 (caller stream only): every pixel, clearing the
+    // flags; part 0 (unsplit pass): every pixel
+    uint8_t *deep_px;
+    uint32_t part;
 };
 
 // RT_FLAG_CUDA_COMPAT: the semantics of the reference's CUDA variant (src/CUDA/cuda_impl.cu),

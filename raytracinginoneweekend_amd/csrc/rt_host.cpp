@@ -204,6 +204,7 @@ struct rt_scene {
     uint32_t *queue_ctr = nullptr;  // kCtrWords: queue and segment counters (layout at kCtrWords)
     hipStream_t xs[kMaxBufs] = {};
     hipEvent_t ev_done[kMaxWs] = {}, ev_free[kMaxWs] = {};
+    hipEvent_t ev_main[kMaxWs] = {};  // split passes: after the main launch (created on first use)
     bool free_valid[kMaxWs] = {};
     // queue/segment counters of workspace b not known to be zero (set while a render using
     // them is enqueued, cleared once the accumulation that resets them is enqueued after it)
@@ -865,6 +866,7 @@ int rt_scene_destroy(rt_scene *sc)
     for (uint32_t b = 0; b < kMaxWs; ++b) {
         if (sc->ev_done[b]) (void)hipEventDestroy(sc->ev_done[b]);
         if (sc->ev_free[b]) (void)hipEventDestroy(sc->ev_free[b]);
+        if (sc->ev_main[b]) (void)hipEventDestroy(sc->ev_main[b]);
     }
     if (sc->ev_tail) (void)hipEventDestroy(sc->ev_tail);
     for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr, sc->wq})
@@ -1240,16 +1242,22 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
         k.deep_depth = 0;
         k.deep_mode = 0;
+        bool two_part = false;
         if (deep_split && !wave && deep_split < P.max_depth && k.n_items >= deep_min_items) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
-            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], static_cast<size_t>(cap) * 48u); rc) return rc;
+            const size_t had = sc->deep_bytes[wb];
+            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], static_cast<size_t>(cap) * 48u + n_pixels); rc) return rc;
+            if (sc->deep_bytes[wb] != had)  // new memory: the pixel flags start cleared
+                RT_HIP(hipMemsetAsync(static_cast<char *>(sc->deep[wb]) + static_cast<size_t>(cap) * 48u, 0, n_pixels, xst));
             char *base = static_cast<char *>(sc->deep[wb]);
             k.deep.f = reinterpret_cast<float *>(base);
             k.deep.rng = reinterpret_cast<uint64_t *>(base + static_cast<size_t>(cap) * 36u);
             k.deep.slot = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 44u);
             k.deep.ctr = k.queue_ctr;
             k.deep.rcap = rcap;
+            k.deep.px = reinterpret_cast<uint8_t *>(base + static_cast<size_t>(cap) * 48u);
             k.deep_depth = deep_split;
+            two_part = pipe && !in_flight;
         }
         if (verbose())
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) %s%u\n",
@@ -1278,6 +1286,10 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             }
         } else {
             RT_HIP(rt::launch_render(variant, cull_mode, k, grid, xst));
+            if (two_part) {
+                if (!sc->ev_main[wb]) RT_HIP(hipEventCreateWithFlags(&sc->ev_main[wb], hipEventDisableTiming));
+                RT_HIP(hipEventRecord(sc->ev_main[wb], xst));
+            }
             if (k.deep_depth) {  // the deep launch: the queued paths, same grid, same stream
                 rt::KParams kd = k;
                 kd.deep_mode = k.deep_depth;
@@ -1293,7 +1305,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], xst));
         if (pipe) {
             RT_HIP(hipEventRecord(sc->ev_done[wb], xst));
-            RT_HIP(hipStreamWaitEvent(st, sc->ev_done[wb], 0));
             sc->last_ws = static_cast<int>(wb);
         }
         rt::KAccum a{};
@@ -1322,6 +1333,26 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             a.deep_key = deep_key;
             a.deep_rcap = k.deep.rcap;
         }
+        if (two_part) {
+            // a pass issued while no other render runs (a lone frame, the first of a stream):
+            // the pixels without deep samples accumulate beside the deep launch, the others (and
+            // the counters) after it. In a frame stream the other frames' work fills that time,
+            // and the extra launch per pass measured ~1% slower there.
+            rt::KAccum a1 = a;
+            a1.seg_from = a1.seg_to = nullptr;
+            a1.queue_reset = nullptr;
+            a1.deep_over = nullptr;
+            a1.deep_px = k.deep.px;
+            a1.part = 1;
+            RT_HIP(hipStreamWaitEvent(st, sc->ev_main[wb], 0));
+            RT_HIP(rt::launch_accumulate(a1, st));
+            a.deep_px = k.deep.px;
+            a.part = 2;
+        } else if (k.deep_depth) {
+            a.deep_px = k.deep.px;  // one part; clears the flags the main launch set
+            a.part = 3;
+        }
+        if (pipe) RT_HIP(hipStreamWaitEvent(st, sc->ev_done[wb], 0));
         RT_HIP(rt::launch_accumulate(a, st));
         sc->ctr_dirty[wb] = false;
         if (pipe) {

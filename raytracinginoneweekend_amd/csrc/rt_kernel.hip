@@ -982,6 +982,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     f[6 * cap + j] = att.x; f[7 * cap + j] = att.y; f[8 * cap + j] = att.z;
                     p.deep.rng[j] = rng;
                     p.deep.slot[j] = ls * fc->n_pixels + pix;
+                    p.deep.px[pix] = 1;
                     alive = false;
                 }
             }
@@ -1392,6 +1393,14 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
             k.queue_reset[w] = 0u;
         }
     if (i >= k.n_pixels) return;
+    // split passes (KAccum::part): 1 = pixels without deep samples, 2 = the others, 3 = all
+    // pixels in one part; 2 and 3 clear the flags for the workspace's next pass
+    if (k.part) {
+        const bool flagged = k.deep_px[i];
+        if (k.part == 1 && flagged) return;
+        if (k.part == 2 && !flagged) return;
+        if (k.part != 1 && flagged) k.deep_px[i] = 0;
+    }
     f3 acc;
     if (k.first) acc = mk(0.f, 0.f, 0.f);
     else acc = mk(k.acc[3 * i], k.acc[3 * i + 1], k.acc[3 * i + 2]);

@@ -422,7 +422,7 @@ def main():
                        # deep-path split: split depth, and the pass size below which
                        # passes are not split (library defaults unless set in the environment)
                        "deep_split": int(os.environ.get("RT_DEEP_SPLIT", "8")),
-                       "deep_min_items": int(os.environ.get("RT_DEEP_MIN_ITEMS", str(1 << 26)))},
+                       "deep_min_items": int(os.environ.get("RT_DEEP_MIN_ITEMS", str(1 << 25)))},
             # ms_per_step is the steady-state period of a frame stream (frames in flight);
             # frame_wall_ms is ONE frame alone, start to finish (render, accumulate, gather)
             "frame_wall_ms": r3(main_m["frame_latency_ms"]),

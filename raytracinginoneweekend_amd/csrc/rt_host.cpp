@@ -711,7 +711,7 @@ uint32_t deep_split_env()
 }
 // deep queue of a pass: 8 regions of 1/1024 of its samples each (at least 512): 0.8% of the
 // samples, where 0.2-0.3% reach the split depth on config 3; paths past a full region stay in the
-// main launch. Passes of fewer than RT_DEEP_MIN_ITEMS samples (default 2^26) are not split: the
+// main launch. Passes of fewer than RT_DEEP_MIN_ITEMS samples (default 2^25) are not split: the
 // deep launch is a serial tail of about max_depth - split iterations, which a small pass's own
 // drain does not outweigh (config 3's 8-way row share: 0.58-0.65 vs 0.52 ms per frame).
 uint32_t deep_region_cap(uint32_t n_items)
@@ -740,7 +740,7 @@ unsigned long long camera_key(const rt_camera &c, uint32_t max_depth)
 uint64_t deep_min_items_env()
 {
     const char *e = std::getenv("RT_DEEP_MIN_ITEMS");
-    return e && *e ? std::strtoull(e, nullptr, 10) : (1ull << 26);
+    return e && *e ? std::strtoull(e, nullptr, 10) : (1ull << 25);
 }
 
 } // namespace

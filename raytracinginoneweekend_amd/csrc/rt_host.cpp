@@ -1243,7 +1243,10 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.deep_depth = 0;
         k.deep_mode = 0;
         bool two_part = false;
-        if (deep_split && !wave && deep_split < P.max_depth && k.n_items >= deep_min_items) {
+        // culled scenes only: with a handful of spheres (the simple scene, brute force) a deep
+        // segment is cheap and the deep launch's overhead outweighs the drain it saves
+        // (config 2: 0.98-1.00 vs 0.98-0.99 ms per frame)
+        if (deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth && k.n_items >= deep_min_items) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
             const size_t had = sc->deep_bytes[wb];
             if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], static_cast<size_t>(cap) * 48u + n_pixels); rc) return rc;

@@ -299,9 +299,10 @@ def test_deep_split_overflow_feedback(monkeypatch):
 
 @pytest.mark.parametrize("pipeline", ["", "0"])
 def test_deep_split_variants_and_row_shares(pipeline, monkeypatch):
-    """The split with every render variant it applies to (fast-math, brute force, the scalar-cache
-    scene, the simple scene's brute-force walk), on the caller's stream alone (RT_PIPELINE=0) or
-    on the render streams, and for interleaved row shares: each equals its unsplit render."""
+    """The split with the render variants (fast-math; brute force, the scalar-cache scene and the
+    simple scene, which walk every sphere and are not split), on the caller's stream alone
+    (RT_PIPELINE=0) or on the render streams, and for interleaved row shares: each equals its
+    unsplit render."""
     monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
     monkeypatch.setenv("RT_PIPELINE", pipeline)
     W, H, spp = 72, 40, 8

@@ -12,8 +12,12 @@ internal stream with its own workspace; results still land in caller-stream orde
 so ms_per_step is the steady-state frame time; frame_latency_ms is one frame alone, start to
 finish (render + accumulate + gather), timed synchronously after the timed loop.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]     (N > 1: starts N ranks itself)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+parity: rank 0 hashes the last timed frame and compares it with the reference's own whole-frame
+digest (tests/golden/fullframe.json, made from the reference's CPU path by
+tests/golden/make_fullframe.py): "matches_reference" is true only if every bit agrees.
 
 The cpu_baseline leg (rank 0, N=1) times the REFERENCE's own CPU path (oracle/_ref, built
 from /root/reference) on a bounded row subset of the same workload, on this host's cores, with
@@ -85,7 +89,8 @@ def parse():
                     help="f32: the linear frame (12 B/pixel gathered); rgb8: gamma/u8 epilogue on every rank "
                          "before the gather (3 B/pixel), the reference's output format")
     ap.add_argument("--digest", action="store_true",
-                    help="add frame_sha256, the sha256 of the last frame's bytes on rank 0 (A/B bit checks)")
+                    help="kept for old scripts: every line now carries parity.frame_sha256 (the last timed frame's "
+                         "sha256 on rank 0) and its comparison with the reference's digest")
     ap.add_argument("--corrected-steps", type=int, default=5,
                     help="frames of the same workload with the corrected camera, reported as corrected_camera "
                          "(0: skip)")
@@ -95,7 +100,79 @@ def parse():
                          "de-interleave copy), to see whether that work waits for CU slots")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_render_c3.json"),
                     help="PMC summary of this kernel (scripts/pmc_round.sh) for roofline.traffic / VALU busy")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher self-test (CPU): every rank joins a gloo group, prints its rank/world and "
+                         "exits before any GPU call")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` started as ONE process: run N ranks under torch.distributed.run (one
+    process per GPU, rendezvous on 127.0.0.1) and return its exit code. Called before this
+    process touches the GPU (it never initialises HIP), so the ranks start clean."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the host driver's only mode)
+    env.setdefault("OMP_NUM_THREADS", env.get("OMP_NUM_THREADS", "16"))
+    return subprocess.call(cmd, env=env)
+
+
+def env_int(name, default):
+    """An integer from the environment, empty meaning the default (as rt_host.cpp reads it)."""
+    v = os.environ.get(name, "")
+    try:
+        return int(v) if v.strip() else default
+    except ValueError:
+        return default
+
+
+def reference_digest(config, W, H):
+    """The reference's whole-frame digests for this config (tests/golden/fullframe.json, made by
+    tests/golden/make_fullframe.py from the reference's own CPU path), or None."""
+    try:
+        with open(os.path.join(REPO, "tests", "golden", "fullframe.json")) as f:
+            rec = json.load(f).get(config)
+    except (OSError, ValueError):
+        return None
+    return rec if rec and rec["width"] == W and rec["height"] == H else None
+
+
+def parity_record(frame_np, config, W, H, row_offset, row_stride, seed, camera, variant, output):
+    """Compare the last timed frame (rank 0) with the reference's digests: the whole frame's
+    sha256, or for a row share (rehearsal) the 64-bit row digests of the rows it rendered."""
+    import hashlib
+    rows = frame_np.shape[0]
+    rec = {"frame_sha256": hashlib.sha256(frame_np.tobytes()).hexdigest()}
+    ref = reference_digest(config, W, H)
+    if output != "f32":
+        rec.update(matches_reference=None, note="u8 output: the device epilogue is within 1 LSB of glibc powf, "
+                                                "not bitwise; the f32 frame is the parity object")
+        return rec
+    if ref is None or seed != ref["seed"] or camera != ref["camera"]:
+        rec.update(matches_reference=None, note="no reference digest for this config/seed/camera")
+        return rec
+    if row_stride == 1 and rows == ref["height"]:
+        rec["reference_sha256"] = ref["sha256_f32"]
+        rec["matches_reference"] = rec["frame_sha256"] == ref["sha256_f32"]
+    else:
+        got = [hashlib.sha256(frame_np[i].tobytes()).hexdigest()[:16] for i in range(rows)]
+        want = [ref["row_sha256_16"][row_offset + i * row_stride] for i in range(rows)]
+        bad = [row_offset + i * row_stride for i in range(rows) if got[i] != want[i]]
+        rec.update(rows_checked=rows, rows_differing=len(bad), matches_reference=not bad)
+    if variant == "fast":
+        rec["note"] = "fast variant: within the stated tolerance, not bitwise by design"
+    rec["reference"] = "tests/golden/fullframe.json[%s] (oracle/_ref/ref_harness_pcg, the reference's CPU path)" % config
+    return rec
 
 
 def lib_sha256():
@@ -260,19 +337,41 @@ def cpu_baseline(cfg, camera, seed, rows, threads):
         **host)
 
 
+def launch_check(world, rank, local):
+    """--launch-check: the rank joins a gloo group, agrees on the world with an all-reduce and
+    prints one JSON line; no GPU call (tests/test_bench_launcher.py)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([rank], dtype=torch.int64)
+        dist.all_reduce(t)
+        total = int(t.item())
+        dist.destroy_process_group()
+    else:
+        total = 0
+    print(json.dumps({"launch_check": True, "rank": rank, "local_rank": local, "world": world,
+                      "rank_sum": total, "master_addr": os.environ.get("MASTER_ADDR")}), flush=True)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process started with --gpus N: become the launcher of N ranks (before any HIP call)
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launch_check:
+        return launch_check(world, rank, local)
     hw_env = os.environ.get("GPU_MAX_HW_QUEUES")
     if args.hw_queues > 0:  # before anything starts HIP: 8 queues -> 4 render streams
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1:
-        raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
     distributed = world > 1
     torch.cuda.set_device(local)
     if distributed:
@@ -304,11 +403,23 @@ def main():
         fake = torch.empty((rehearse, rows, W, 3), dtype=torch.float32, device=dev)
         frame_r = torch.empty((rows * rehearse, W, 3), dtype=torch.float32, device=dev)
 
-    def measure(cam, steps, warmup):
+    def out_frame():
+        """rank 0's output of a step: the gathered frame (N > 1) or its own tile."""
+        return gather.frame if (world > 1 and not rehearse) else (tile8 if rgb8 else tile)
+
+    # the reference's entry returns the frame in host memory (cuda_impl.cu:449-452): the frame
+    # wall clock ends with the device->host copy into a pinned buffer (SURVEY §8(d))
+    host_frame = torch.empty(out_frame().shape, dtype=out_frame().dtype, pin_memory=True) if rank == 0 else None
+    parity = {}
+
+    def measure(cam, steps, warmup, check_parity=False):
         """warmup untimed frames, then `steps` frames timed between barriers + syncs (max over
-        ranks), then one frame alone three times (its latency, median), then one frame of the
-        counting kernel (the same paths and bits, plus tallies of segments and executed tests:
-        the work of every frame of this workload, which the timed frames do not tally)."""
+        ranks), then one frame alone three times on the device (its latency, median) and three
+        times including the copy of the frame to host memory (the frame wall clock), then one
+        frame of the counting kernel (the same paths and bits, plus tallies of segments and
+        executed tests: the work of every frame of this workload, which the timed frames do not
+        tally). check_parity: rank 0 compares the last timed frame with the reference's digests
+        (outside the timed region)."""
         def step(count_segments):
             ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
             if rgb8:
@@ -335,16 +446,24 @@ def main():
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         spans = ds.kernel_times(steps)  # HIP-event spans of the timed frames' render launches
-        lat = []
-        for _ in range(3):
-            torch.cuda.synchronize()
-            if distributed:
-                dist.barrier()
-            t1 = time.perf_counter()
-            step(False)
-            torch.cuda.synchronize()
-            lat.append(time.perf_counter() - t1)
-        latency = sorted(lat)[1]
+        if check_parity and rank == 0:
+            frame = out_frame().cpu().numpy()
+            off, stride = (0, 1) if not rehearse else (params.row_offset, params.row_stride)
+            parity.update(parity_record(frame, args.config, W, H, off, stride, args.seed, args.camera,
+                                        args.variant, args.output))
+        lat, wall = [], []
+        for to_host in (False, True):
+            for _ in range(3):
+                torch.cuda.synchronize()
+                if distributed:
+                    dist.barrier()
+                t1 = time.perf_counter()
+                step(False)
+                if to_host and rank == 0:
+                    host_frame.copy_(out_frame(), non_blocking=True)
+                torch.cuda.synchronize()
+                (wall if to_host else lat).append(time.perf_counter() - t1)
+        latency, wall_clock = sorted(lat)[1], sorted(wall)[1]
         torch.cuda.synchronize()
         seg.zero_()
         step(True)
@@ -352,15 +471,16 @@ def main():
         counts = [int(x) * steps for x in seg.tolist()]  # per frame x timed frames
         counts_all = counts
         if distributed:
-            t = torch.tensor([elapsed, latency], dtype=torch.float64, device=dev)
+            t = torch.tensor([elapsed, latency, wall_clock], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed, latency = float(t[0].item()), float(t[1].item())
+            elapsed, latency, wall_clock = float(t[0].item()), float(t[1].item()), float(t[2].item())
             sg = seg.clone()
             dist.all_reduce(sg)
             counts_all = [int(x) for x in sg.tolist()]
-        return elapsed, latency, spans, counts, counts_all
+        return elapsed, (latency, wall_clock), spans, counts, counts_all
 
-    def summary(elapsed, latency, spans, counts, counts_all, steps):
+    def summary(elapsed, lat_wall, spans, counts, counts_all, steps):
+        latency, wall_clock = lat_wall
         segments, sph_tests, box_tests = counts
         primaries = (W * rows if rehearse else W * H) * spp * steps
         period = elapsed / steps
@@ -371,6 +491,7 @@ def main():
         span = sum(spans) / max(len(spans), 1)
         return {
             "value": primaries / elapsed / 1e6, "ms_per_step": period * 1e3, "frame_latency_ms": latency * 1e3,
+            "frame_wall_ms": wall_clock * 1e3,
             "segments_per_primary": counts_all[0] / primaries,
             "msegments_per_s": counts_all[0] / elapsed / 1e6,
             "gtests_per_s": counts_all[1] / elapsed / 1e9, "gbox_tests_per_s": counts_all[2] / elapsed / 1e9,
@@ -383,13 +504,7 @@ def main():
 
     mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
     cam = rt.Camera.cuda(W, H) if compat else rt.Camera.default(W, H, mode)
-    main_m = summary(*measure(cam, args.steps, args.warmup), args.steps)
-    digest = None
-    if args.digest and rank == 0:
-        import hashlib
-        torch.cuda.synchronize()
-        frame = gather.frame if (world > 1 and not rehearse) else (tile8 if rgb8 else tile)
-        digest = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()
+    main_m = summary(*measure(cam, args.steps, args.warmup, check_parity=not compat), args.steps)
     corr = None
     if args.corrected_steps > 0 and not compat and args.camera == "reference":
         # the representative path-tracing load (7 segments per primary): the corrected camera
@@ -421,11 +536,15 @@ def main():
                        "hw_queues_env": hw_env,
                        # deep-path split: split depth, and the pass size below which
                        # passes are not split (library defaults unless set in the environment)
-                       "deep_split": int(os.environ.get("RT_DEEP_SPLIT", "8")),
-                       "deep_min_items": int(os.environ.get("RT_DEEP_MIN_ITEMS", str(1 << 25)))},
+                       "deep_split": env_int("RT_DEEP_SPLIT", 8),
+                       "deep_min_items": env_int("RT_DEEP_MIN_ITEMS", 1 << 25)},
             # ms_per_step is the steady-state period of a frame stream (frames in flight);
-            # frame_wall_ms is ONE frame alone, start to finish (render, accumulate, gather)
-            "frame_wall_ms": r3(main_m["frame_latency_ms"]),
+            # frame_wall_ms is ONE frame alone, start to finish, ending with the frame in host
+            # memory as the reference's entry returns it (render, accumulate, gather, D2H copy
+            # into pinned memory); frame_device_ms is the same frame without the copy (the
+            # round-2 "frame_wall_ms"/"frame_latency_ms")
+            "frame_wall_ms": r3(main_m["frame_wall_ms"]),
+            "frame_device_ms": r3(main_m["frame_latency_ms"]),
             "frame_latency_ms": r3(main_m["frame_latency_ms"]),
             "frames_in_flight": frames_in_flight(),
             "segments_per_primary": round(main_m["segments_per_primary"], 4),
@@ -456,6 +575,8 @@ def main():
         kname = f"render_kernel<{v}, {cull}, false, false>"
         pmc, status = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
                                                    "traversal": args.traversal, "n_gpus": world})
+        if args.variant == "wavefront":  # other kernels did the work: no render_kernel PMC
+            pmc, status = None, "other kernels (wave_gen_kernel, wave_bounce_kernel)"
         rec["roofline"]["pmc_status"] = status
         if pmc and not rehearse:
             # HBM bytes per frame (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE, one
@@ -467,8 +588,8 @@ def main():
             rec["roofline"]["valu_busy"] = round(
                 pmc["valu_insts"] * 2.0 / (1024 * pmc["clock_ghz"] * 1e9 * main_m["ms_per_step"] * 1e-3), 4)
             rec["roofline"]["pmc_source"] = os.path.relpath(args.pmc, REPO)
-        if digest:
-            rec["frame_sha256"] = digest
+        if parity:
+            rec["parity"] = parity
         if corr:
             rec["corrected_camera"] = {
                 "value": round(corr["value"], 3), "unit": "Mrays/s", "steps": args.corrected_steps,

@@ -248,7 +248,8 @@ int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixel
  * the caller's frame. Scenes, streams and communicators are built once here; tiles and the
  * gather buffer are allocated on first use of a frame size. Ranks that share a device with
  * rank 0 ("virtual ranks", e.g. devices = {0, 0, 0, 0}: an N-way split rehearsed on one
- * GPU) move their tiles with device copies instead of RCCL; the result is the same frame.  */
+ * GPU) move their tiles with device copies instead of RCCL; the result is the same frame.
+ * A device list is either all distinct or all equal to devices[0]; a mix is RT_ERR_INVALID. */
 typedef struct rt_multi rt_multi;
 enum rt_output_format { RT_OUTPUT_F32 = 0, RT_OUTPUT_RGB8 = 1 };
 int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres,

@@ -192,12 +192,18 @@ struct rt_scene {
     size_t slots_bytes[kMaxWs] = {};
     float *acc = nullptr;
     size_t acc_bytes = 0;
-    void *deep[kMaxWs] = {};  // deep-path split: the deep queue of each workspace (rt::DeepQueue)
-    size_t deep_bytes[kMaxWs] = {};
+    // deep-path split: per workspace, the pixel flags (a byte per pixel, at the front) and then
+    // the deep queue (rt::DeepQueue); deep_clean = leading bytes known to be zero (every pass's
+    // accumulation clears the flags it set, so only a larger pixel count needs a memset)
+    void *deep[kMaxWs] = {};
+    size_t deep_bytes[kMaxWs] = {}, deep_clean[kMaxWs] = {};
     // deep-queue overflow reports (pinned host memory written by accumulate_kernel, one word per
-    // workspace) and the camera keys they named: renders with such a camera are not split
+    // workspace) and the camera keys they named, with the call that last reported each: renders
+    // with such a camera are not split for kDeepOffCalls calls; at most kDeepOffKeys keys (LRU)
     unsigned long long *deep_over = nullptr, *deep_over_dev = nullptr;
-    std::vector<unsigned long long> deep_off;
+    static constexpr size_t kDeepOffKeys = 8;
+    static constexpr uint64_t kDeepOffCalls = 256;
+    std::vector<std::pair<unsigned long long, uint64_t>> deep_off;
     void *wq = nullptr;  // RT_FLAG_WAVEFRONT: two ray queues and their counters
     size_t wq_bytes = 0;
     int occ_wave[2] = {-1, -1};  // wave_bounce_kernel blocks per CU [culled], -1 = unknown
@@ -1156,14 +1162,21 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // queue on this scene: paths that long are common there (the corrected camera: 8.4% of the
     // samples pass 8 segments, 59% of the segments), and a partial split only adds a tail
     for (uint32_t w = 0; w < kMaxWs; ++w) {
-        const unsigned long long v = reinterpret_cast<volatile unsigned long long *>(sc->deep_over)[w];
-        if (v) {
-            if (std::find(sc->deep_off.begin(), sc->deep_off.end(), v) == sc->deep_off.end()) sc->deep_off.push_back(v);
-            reinterpret_cast<volatile unsigned long long *>(sc->deep_over)[w] = 0ull;
-        }
+        // take-and-clear in one atomic step: a report the device writes meanwhile is kept
+        const unsigned long long v = __atomic_exchange_n(sc->deep_over + w, 0ull, __ATOMIC_ACQ_REL);
+        if (!v) continue;
+        auto it = std::find_if(sc->deep_off.begin(), sc->deep_off.end(), [&](const auto &e) { return e.first == v; });
+        if (it != sc->deep_off.end()) sc->deep_off.erase(it);
+        else if (sc->deep_off.size() >= rt_scene::kDeepOffKeys) sc->deep_off.erase(sc->deep_off.begin());
+        sc->deep_off.emplace_back(v, sc->calls);  // most recent last
     }
+    // reports expire: a camera is tried split again kDeepOffCalls calls after its last overflow
+    sc->deep_off.erase(std::remove_if(sc->deep_off.begin(), sc->deep_off.end(),
+                                      [&](const auto &e) { return sc->calls - e.second > rt_scene::kDeepOffCalls; }),
+                       sc->deep_off.end());
     const unsigned long long deep_key = camera_key(*camera, P.max_depth);
-    const bool deep_off = std::find(sc->deep_off.begin(), sc->deep_off.end(), deep_key) != sc->deep_off.end();
+    const bool deep_off = std::find_if(sc->deep_off.begin(), sc->deep_off.end(),
+                                       [&](const auto &e) { return e.first == deep_key; }) != sc->deep_off.end();
     const uint32_t deep_split = deep_off ? 0u : deep_split_env();
     const uint64_t deep_min_items = deep_min_items_env();
     const uint32_t bufs = wave ? 1u : pipeline_env();  // the wavefront variant: caller stream only
@@ -1248,17 +1261,22 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         // (config 2: 0.98-1.00 vs 0.98-0.99 ms per frame)
         if (deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth && k.n_items >= deep_min_items) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
-            const size_t had = sc->deep_bytes[wb];
-            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], static_cast<size_t>(cap) * 48u + n_pixels); rc) return rc;
-            if (sc->deep_bytes[wb] != had)  // new memory: the pixel flags start cleared
-                RT_HIP(hipMemsetAsync(static_cast<char *>(sc->deep[wb]) + static_cast<size_t>(cap) * 48u, 0, n_pixels, xst));
+            const size_t px_bytes = (n_pixels + 255u) & ~static_cast<size_t>(255u);
+            void *had = sc->deep[wb];
+            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], px_bytes + static_cast<size_t>(cap) * 48u); rc) return rc;
+            if (sc->deep[wb] != had) sc->deep_clean[wb] = 0;  // new memory
+            if (sc->deep_clean[wb] < px_bytes) {  // flags over bytes a queue may have used
+                RT_HIP(hipMemsetAsync(sc->deep[wb], 0, px_bytes, xst));
+                sc->deep_clean[wb] = px_bytes;
+            }
             char *base = static_cast<char *>(sc->deep[wb]);
+            k.deep.px = reinterpret_cast<uint8_t *>(base);
+            base += px_bytes;
             k.deep.f = reinterpret_cast<float *>(base);
             k.deep.rng = reinterpret_cast<uint64_t *>(base + static_cast<size_t>(cap) * 36u);
             k.deep.slot = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 44u);
             k.deep.ctr = k.queue_ctr;
             k.deep.rcap = rcap;
-            k.deep.px = reinterpret_cast<uint8_t *>(base + static_cast<size_t>(cap) * 48u);
             k.deep_depth = deep_split;
             two_part = pipe && !in_flight;
         }
@@ -1638,8 +1656,8 @@ namespace {
 
 int multi_fail_destroy(rt_multi *m, int rc);
 
-// ensure() without the device-wide synchronisation: the buffers of a context grow only
-// between frames the caller has already synchronised (rt_multi_render_* documents it)
+// ensure() on a given device. Growing reallocates and so synchronises that device; the
+// buffers of a context grow only when a frame is larger than any before it (rt_api.h)
 int grow(int device, void **ptr, size_t *have, size_t want)
 {
     if (*have >= want && *ptr) return RT_OK;
@@ -1684,10 +1702,18 @@ int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         }
         m->dev.push_back(d);
     }
-    m->rccl = N > 1;
-    for (int r = 0; r < N && m->rccl; ++r)
-        for (int q = 0; q < r; ++q)
-            if (m->dev[q] == m->dev[r]) m->rccl = false;
+    // two supported layouts: every rank on its own device (RCCL), or every rank on rank 0's
+    // device (virtual ranks); a mix would gather through cross-device copies no test covers
+    bool distinct = true, all_same = true;
+    for (int r = 1; r < N; ++r) {
+        all_same = all_same && m->dev[r] == m->dev[0];
+        for (int q = 0; q < r; ++q) distinct = distinct && m->dev[q] != m->dev[r];
+    }
+    if (!distinct && !all_same) {
+        delete m;
+        return fail(RT_ERR_INVALID, "rt_multi_create: devices must be all distinct or all rank 0's device");
+    }
+    m->rccl = N > 1 && distinct;
     m->sc.assign(N, nullptr);
     m->st.assign(N, nullptr);
     m->tile.assign(N, nullptr);

@@ -19,7 +19,8 @@ step() {  # step <name> <seconds> <cmd...>
 for s in ${STEPS:-smoke pytest bench prof}; do
   case $s in
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) step pytest 900 python -m pytest tests -m gpu -x -q ;;
+    pytest) step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
+    stock)  step stock 600 python bench.py --hw-queues 0 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     ab)     step ab 900 python scripts/ab_variants.py --rounds ${AB_ROUNDS:-5} --variants ${AB_VARIANTS:-exact:cull,fast:cull} ;;
     abl)    RT_LIB_PATH=$PWD/scripts/_abl/librt_mi355x.so step abl 900 python scripts/ab_variants.py --rounds ${AB_ROUNDS:-5} --variants ${AB_VARIANTS:-exact:cull,fast:cull} ;;

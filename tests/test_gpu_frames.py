@@ -6,6 +6,8 @@ the PPM writer, and renders whose caller stream changes between calls.
 Tolerance: f32 bitwise (0 ULP), as tests/test_gpu_parity.py; u8 within 1 LSB on a handful of
 texels (device pow vs glibc powf).
 """
+import hashlib
+import json
 import os
 
 import numpy as np
@@ -44,6 +46,51 @@ FULL = {
 }
 
 
+def _full_ref(cfg):
+    """The reference's whole-frame digests (tests/golden/make_fullframe.py)."""
+    with open(os.path.join(G.GOLDEN, "fullframe.json")) as f:
+        return json.load(f)[cfg]
+
+
+def _assert_frame_digest(img, ref, what):
+    """Whole f32 frame == the reference's, bit for bit; on a mismatch name the rows."""
+    got = hashlib.sha256(np.ascontiguousarray(img, dtype=np.float32).tobytes()).hexdigest()
+    if got != ref["sha256_f32"]:
+        bad = [y for y in range(img.shape[0])
+               if hashlib.sha256(img[y].tobytes()).hexdigest()[:16] != ref["row_sha256_16"][y]]
+        raise AssertionError(f"{what}: frame differs from the reference in {len(bad)} of {img.shape[0]} rows, "
+                             f"first {bad[:8]}")
+
+
+# ---- configs 2 and 3 (the headline) whole, through the bench's frames-in-flight path -------
+@pytest.mark.parametrize("cfg", ["c3", "c2"])
+def test_baseline_frame_stream_matches_reference(cfg):
+    """BASELINE configs 3 (huge scene 1280x720 @128 spp, the bench's workload) and 2 (simple
+    scene 1280x720 @64 spp, depth 50), rendered as bench.py renders them: DeviceScene.render
+    into device buffers, frames back to back on one stream without host sync (renders on the
+    internal streams, partial grids while others run, the deep-path split at its defaults,
+    two-part accumulation for the lone first frame), then a counting frame. Every frame's
+    whole f32 image must equal the reference's own render of the full frame
+    (oracle/_ref/ref_harness_pcg, src/main.cxx:185-215), compared by sha256."""
+    torch = pytest.importorskip("torch")
+    ref = _full_ref(cfg)
+    W, H, spp, depth = ref["width"], ref["height"], ref["spp"], ref["depth"]
+    s, m = G.scene(ref["scene"])
+    ds = rt.DeviceScene((s, m))
+    p = rt.make_params(W, H, spp, depth, ref["seed"])
+    cam = rt.Camera.default(W, H)
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(5)]
+    seg = torch.zeros(3, dtype=torch.int64, device="cuda")
+    for k, o in enumerate(outs):
+        ds.render(cam, p, o.data_ptr(), stream, seg.data_ptr() if k == len(outs) - 1 else None)
+    torch.cuda.synchronize()
+    ds.close()
+    for k, o in enumerate(outs):
+        _assert_frame_digest(o.cpu().numpy(), ref, f"{cfg} frame {k}")
+    assert int(seg[0]) > W * H * spp  # every primary plus its bounces
+
+
 @pytest.mark.parametrize("cfg", sorted(FULL))
 def test_full_config_frame_matches_reference_rows(cfg):
     c = FULL[cfg]
@@ -51,6 +98,11 @@ def test_full_config_frame_matches_reference_rows(cfg):
     s, m = G.scene("huge")
     img, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 1234, full_frame=True))
     assert st.primaries == W * H * spp
+    # the whole frame against the reference's own full render, when its digest is committed
+    try:
+        _assert_frame_digest(img, _full_ref(cfg), cfg)
+    except KeyError:
+        pass
     # the reference's own row (tests/golden/make_golden.py, oracle/_ref)
     meta, f32, u8 = G.render(c["golden"])
     y = meta["row_offset"]
@@ -318,3 +370,30 @@ def test_deep_split_variants_and_row_shares(pipeline, monkeypatch):
         b, sb = rt.render_f32((s, m), p, cam)
         _bits_equal(b, a, f"{scene} {kw} {rows}")
         assert sb.segments == sa.segments
+
+
+def test_deep_split_streams_passes_of_changing_size(monkeypatch):
+    """One DeviceScene, split passes of different pixel and sample counts streamed without host
+    sync, so every workspace's deep-queue buffer serves passes of other sizes (its pixel flags
+    must start cleared whatever the previous pass left there: rt_host.cpp deep_clean). Each
+    frame equals its unsplit render, bit for bit, with the same segment count."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
+    monkeypatch.setenv("RT_DEEP_SPLIT", "2")
+    s, m = G.scene("huge")
+    sizes = [(160, 90, 16), (48, 27, 3), (200, 120, 8), (64, 36, 4), (96, 54, 12), (40, 20, 5)] * 3
+    ds = rt.DeviceScene((s, m))
+    stream = torch.cuda.current_stream().cuda_stream
+    outs, segs = [], []
+    for k, (W, H, spp) in enumerate(sizes):
+        outs.append(torch.empty((H, W, 3), dtype=torch.float32, device="cuda"))
+        segs.append(torch.zeros(3, dtype=torch.int64, device="cuda"))
+        ds.render(rt.Camera.default(W, H, k % 2), rt.make_params(W, H, spp, 64, 30 + k), outs[-1].data_ptr(),
+                  stream, segs[-1].data_ptr())
+    torch.cuda.synchronize()
+    ds.close()
+    monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+    for k, (W, H, spp) in enumerate(sizes):
+        want, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 30 + k), rt.Camera.default(W, H, k % 2))
+        _bits_equal(outs[k].cpu().numpy(), want, f"frame {k} {W}x{H}@{spp}")
+        assert int(segs[k][0]) == st.segments

@@ -12,6 +12,13 @@ The frames themselves (11-100 MB) are not committed: they are data the tests re-
 on the GPU and compare by digest.
 
     python tests/golden/make_fullframe.py [c2 c3 c5 c4]     # needs /root/reference (build_ref.sh)
+    python tests/golden/make_fullframe.py --dropin
+
+--dropin: the frame the reference's own main() renders in its debug build (src/main.cxx:23-27:
+512x256, 16 spp, simple scene, depth 64), written by the reference's app::save_to_file
+(main.cxx:87-101) to dropin_simple_512x256_s16.ppm, with its digests in dropin.json — what
+examples/_ref/ref_main_dropin (the reference's main() with the INTEGRATION.md swap,
+examples/build_ref_dropin.sh) must reproduce on the GPU.
 """
 import hashlib
 import json
@@ -37,7 +44,28 @@ CONFIGS = {
 }
 
 
+def dropin():
+    W, H, spp = 512, 256, 16
+    ppm = os.path.join(HERE, "dropin_simple_512x256_s16.ppm")
+    with tempfile.TemporaryDirectory() as td:
+        f32p, u8p = os.path.join(td, "f.f32"), os.path.join(td, "f.u8")
+        subprocess.run([EXE, "--scene", "simple", "--w", str(W), "--h", str(H), "--spp", str(spp), "--depth", "64",
+                        "--seed", "1234", "--camera", "reference", "--threads", str(os.cpu_count() or 8),
+                        "--out-f32", f32p, "--out-u8", u8p, "--out-ppm", ppm], check=True)
+        f32 = open(f32p, "rb").read()
+        u8 = open(u8p, "rb").read()
+    rec = {"scene": "simple", "width": W, "height": H, "spp": spp, "depth": 64, "camera": "reference", "seed": 1234,
+           "rng": "pcg", "ppm": os.path.basename(ppm), "sha256_ppm": hashlib.sha256(open(ppm, "rb").read()).hexdigest(),
+           "sha256_f32": hashlib.sha256(f32).hexdigest(), "sha256_u8": hashlib.sha256(u8).hexdigest(),
+           "generator": "oracle/_ref/ref_harness_pcg --out-ppm (the reference's app::save_to_file)"}
+    with open(os.path.join(HERE, "dropin.json"), "w") as f:
+        json.dump(rec, f, indent=1, sort_keys=True)
+    print("dropin:", rec["sha256_ppm"][:16])
+
+
 def main(argv):
+    if argv == ["--dropin"]:
+        return dropin()
     names = argv or ["c2", "c3", "c5", "c4"]
     threads = str(os.cpu_count() or 8)
     rec = {}

@@ -452,8 +452,8 @@ def main():
             parity.update(parity_record(frame, args.config, W, H, off, stride, args.seed, args.camera,
                                         args.variant, args.output))
         lat, wall = [], []
-        for to_host in (False, True):
-            for _ in range(3):
+        for _ in range(3):  # alternating, so both see the same clocks
+            for to_host in (False, True):
                 torch.cuda.synchronize()
                 if distributed:
                     dist.barrier()

@@ -14,7 +14,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _lines(out):
-    return [json.loads(x) for x in out.splitlines() if x.startswith("{") and "launch_check" in x]
+    """Every JSON object in the ranks' merged stdout (lines of different ranks may interleave)."""
+    dec, recs, i = json.JSONDecoder(), [], out.find("{")
+    while i >= 0:
+        obj, end = dec.raw_decode(out, i)
+        if isinstance(obj, dict) and obj.get("launch_check"):
+            recs.append(obj)
+        i = out.find("{", end)
+    return recs
 
 
 @pytest.mark.parametrize("n", [2, 3])

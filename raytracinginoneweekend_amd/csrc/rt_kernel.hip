@@ -645,6 +645,44 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
     return h;
 }
 
+// ---- hot-first dealing (rt_device.h KParams::plan) ----------------------------------------
+// a wave-uniform word of the plan (device memory written by the previous accumulation)
+__device__ __forceinline__ uint32_t plan_word(const uint32_t *plan, uint32_t i)
+{
+    return __builtin_amdgcn_readfirstlane(plan[i]);
+}
+// 64-item blocks of the hot region of a pass of ns samples: hot pixels (a multiple of 64) x ns
+__device__ __forceinline__ uint32_t plan_hot_blocks(const uint32_t *plan, uint32_t ns)
+{
+    return (plan_word(plan, 0) >> 6) * ns;
+}
+// item I of a pass of ns samples -> (natural pixel enumeration index, sample of the pass ls).
+// Without a plan (or with no hot tile): I = ls * n_pixels + pixel. With one: the hot region's
+// items first, sample-major over the hot pixels, then the others' items, sample-major over the
+// rest; enumeration pixel e is tile perm[e / 64] of the natural order (the untiled remainder
+// rows keep their place). Every (pixel, sample) is reached by exactly one item either way.
+template <class FC>
+__device__ __forceinline__ uint32_t item_pixel(const uint32_t *plan, const FC &fc, uint32_t I, uint32_t ns, uint32_t &ls)
+{
+    const uint32_t nh = plan ? plan_word(plan, 0) : 0u;
+    if (!nh) {
+        ls = udiv(I, fc.div_n_pixels.m, fc.div_n_pixels.l);
+        return I - ls * fc.n_pixels;
+    }
+    const uint32_t n_hot_items = nh * ns;
+    uint32_t e;
+    if (I < n_hot_items) {
+        ls = udiv(I, plan_word(plan, 2), plan_word(plan, 3));
+        e = I - ls * nh;
+    } else {
+        const uint32_t J = I - n_hot_items, nc = fc.n_pixels - nh;
+        ls = udiv(J, plan_word(plan, 4), plan_word(plan, 5));
+        e = nh + (J - ls * nc);
+    }
+    const uint32_t n_tiles = plan_word(plan, 1);
+    return (e >> 6) < n_tiles ? (plan[kPlanHeader + (e >> 6)] << 6) | (e & 63u) : e;
+}
+
 // ---- the megakernel ----------------------------------------------------------------------
 // p[i] read from global memory, named as such (a float4 load from address space 1)
 __device__ __forceinline__ float4 gld4(const float4 *p, uint32_t i)
@@ -696,8 +734,10 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     }
     __shared__ float4 lds_pn[256];  // per lane: a pending metal scatter's normal and roughness
 
-    // wave-uniform cursor over the item space (the deep launch: over the queued paths)
+    // wave-uniform cursor over the item space (the deep launch: over the queued paths); with a
+    // hot-first plan every wave serves the 8 hot queues first (hotq), then the 8 others
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
+    bool hotq = p.plan != nullptr;
     uint32_t cnext = 0, cend = 0;
     bool exhausted = false;
     bool deep_full = false;  // this wave's deep-queue region is full: no more splits
@@ -777,7 +817,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     cnext = q * p.deep.rcap + 64u * c;
                     cend = q * p.deep.rcap + min(64u * c + 64u, nq);
                 } else {
-                if (lane == 0) c = atomicAdd(p.queue_ctr + q * kQueueStride, 1u);
+                if (lane == 0) c = atomicAdd(p.queue_ctr + q * kQueueStride + (hotq ? kHotDeal : 0u), 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
                 if (p.guided_l2b < 0.f) {
                     // guided: queue q owns blocks [qb0, qb1) of 64 items; ticket c takes blocks
@@ -786,9 +826,13 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     // served by few atomics and its last chunks are small. S is the same
                     // function for every wave, so consecutive tickets tile the range; the 2t
                     // term keeps it increasing even if exp2 or the float product is off by an
-                    // ulp (one block at most).
-                    const uint32_t qb0 = (uint32_t)(((uint64_t)p.n_blocks * q) >> 3);
-                    const uint32_t B = (uint32_t)(((uint64_t)p.n_blocks * (q + 1u)) >> 3) - qb0;
+                    // ulp (one block at most). With a plan, the first hot_b blocks (the hot
+                    // tiles' samples) are shared by 8 hot queues that every wave serves first,
+                    // and the 8 queues share the rest.
+                    const uint32_t hot_b = p.plan ? plan_hot_blocks(p.plan, p.sample_end - p.sample_begin) : 0u;
+                    const uint32_t nb = hotq ? hot_b : p.n_blocks - hot_b;
+                    const uint32_t qb0 = (hotq ? 0u : hot_b) + (uint32_t)(((uint64_t)nb * q) >> 3);
+                    const uint32_t B = (uint32_t)(((uint64_t)nb * (q + 1u)) >> 3) - (uint32_t)(((uint64_t)nb * q) >> 3);
                     auto S = [&](uint32_t t) -> uint32_t {
                         const float x = t ? exp2f((float)t * p.guided_l2b) : 1.f;
                         const uint64_t g = (uint64_t)floorf((float)B * (1.f - x)) + 2ull * t;
@@ -797,7 +841,15 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     const uint32_t s0 = S(c);
                     if (s0 >= B) {
                         q = (q + 1u) & 7u;
-                        if (++q_tried == 8u) exhausted = true;
+                        if (++q_tried == 8u) {
+                            if (hotq) {  // every hot queue is dry: the others, from the wave's own
+                                hotq = false;
+                                q_tried = 0;
+                                q = blockIdx.x & 7u;
+                            } else {
+                                exhausted = true;
+                            }
+                        }
                         continue;
                     }
                     cnext = 64u * (qb0 + s0);
@@ -841,8 +893,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     depth = p.deep_mode;
                     alive = true;
                 } else {
-                    ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
-                    pix = I - ls * fc->n_pixels;
+                    pix = item_pixel(p.plan, *fc, I, p.sample_end - p.sample_begin, ls);
                     alive = fresh = true;
                 }
             }
@@ -961,6 +1012,13 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         // Paths are appended to region blockIdx % 8 of the queue (8 counters on separate
         // lines, so the appends of the whole grid do not serialise on one address); a wave
         // that finds its region full stops splitting.
+        if (p.tile_stats) {  // hot-first dealing: count the paths that reach kHotDepth per tile
+            const bool hs = alive && !defer && depth == kHotDepth && (ls & p.hot_sample_mask) == 0u;
+            if (ballot(hs)) {
+                const uint32_t tiled_px = fc->tiled_rows * fc->W;
+                if (hs && pix < tiled_px) atomicAdd(p.tile_stats + (pix >> 6), 1u);
+            }
+        }
         if (p.deep_depth && !deep_full) {
             const bool dv = alive && !defer && depth == p.deep_depth;
             const uint64_t m = ballot(dv);
@@ -1375,6 +1433,80 @@ __global__ __launch_bounds__(256) void compat_kernel(const KCompat p)
     }
 }
 
+// ---- the next hot-first plan (one workgroup of accumulate_kernel) ----------------------------
+// From the tile counters (paths that reached kHotDepth, counted by the renders of this scene
+// and layout; other renders may add to them meanwhile, which only changes the choice): a tile
+// is hot if its counter is non-zero. The flags are snapshotted first (words [kPlanHeader + T,
+// kPlanHeader + 2T) of the plan), so the permutation is built from one consistent choice: hot
+// tiles first, then the others, each in natural order. More than half the tiles hot (long
+// paths everywhere, e.g. the corrected camera): natural order. The counters are halved
+// (rounding down), so a tile stays hot while its paths keep reaching kHotDepth.
+__device__ __forceinline__ UDiv udiv_magic(uint32_t d)  // rt_host.cpp make_udiv
+{
+    UDiv r{0u, 0u};
+    if (d <= 1u) return r;
+    const uint32_t l = 32u - (uint32_t)__clz(d - 1u);
+    r.l = l;
+    r.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1u);
+    return r;
+}
+__device__ void build_plan(const KAccum &k)
+{
+    __shared__ uint32_t s_wave[4];
+    const uint32_t T = k.n_tiles, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    uint32_t *flag = k.plan_out + kPlanHeader + T;
+    // block-wide exclusive prefix of v (256 threads: 4 waves) and the total
+    auto block_scan = [&](uint32_t v, uint32_t &total) -> uint32_t {
+        uint32_t x = v;  // inclusive scan within the wave
+        for (uint32_t off = 1; off < 64u; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63u) s_wave[wv] = x;
+        __syncthreads();
+        uint32_t base = 0;
+        for (uint32_t w = 0; w < wv; ++w) base += s_wave[w];
+        total = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        __syncthreads();
+        return base + x - v;
+    };
+    // 1. snapshot the flags (and halve the counters), count the hot tiles
+    uint32_t H = 0;
+    for (uint32_t t0 = 0; t0 < T; t0 += 256u) {
+        const uint32_t t = t0 + tid;
+        uint32_t f = 0;
+        if (t < T) {
+            const uint32_t c = k.tile_stats[t];
+            f = c != 0u;
+            flag[t] = f;
+            if (c) atomicSub(k.tile_stats + t, c - (c >> 1));
+        }
+        uint32_t tot;
+        block_scan(f, tot);
+        H += tot;
+    }
+    if (2u * H > T) H = 0;  // long paths everywhere: natural order
+    // 2. the permutation: position of hot tile t = hot tiles before it; of cold tile t = H + cold before it
+    uint32_t hot_before = 0;
+    for (uint32_t t0 = 0; t0 < T; t0 += 256u) {
+        const uint32_t t = t0 + tid;
+        const uint32_t f = (t < T && H) ? flag[t] : 0u;
+        uint32_t tot;
+        const uint32_t hb = hot_before + block_scan(f, tot);
+        if (t < T) k.plan_out[kPlanHeader + (f ? hb : H + (t - hb))] = t;
+        hot_before += tot;
+    }
+    if (tid == 0) {
+        const uint32_t nh = 64u * H;
+        const UDiv dh = udiv_magic(nh), dc = udiv_magic(k.n_pixels - nh);
+        k.plan_out[0] = nh;
+        k.plan_out[1] = T;
+        k.plan_out[2] = dh.m; k.plan_out[3] = dh.l;
+        k.plan_out[4] = dc.m; k.plan_out[5] = dc.l;
+        k.plan_out[6] = 0u; k.plan_out[7] = 0u;
+    }
+}
+
 // ---- ordered accumulation of the slots, average, optional gamma/u8 --------------------
 __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
 {
@@ -1392,6 +1524,10 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
                 *k.deep_over = k.deep_key;
             k.queue_reset[w] = 0u;
         }
+    if (k.plan_out && blockIdx.x == gridDim.x - 1u) {  // the extra workgroup: the next plan
+        build_plan(k);
+        return;
+    }
     if (i >= k.n_pixels) return;
     // split passes (KAccum::part): 1 = pixels without deep samples, 2 = the others, 3 = all
     // pixels in one part; 2 and 3 clear the flags for the workspace's next pass
@@ -1749,7 +1885,7 @@ hipError_t occupancy_compat(int *blocks_per_cu)
 
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream)
 {
-    const uint32_t grid = (k.n_pixels + 255u) / 256u;
+    const uint32_t grid = (k.n_pixels + 255u) / 256u + (k.plan_out ? 1u : 0u);
     hipLaunchKernelGGL(accumulate_kernel, dim3(grid), dim3(256), 0, stream, k);
     return hipGetLastError();
 }

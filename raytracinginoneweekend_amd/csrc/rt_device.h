@@ -56,23 +56,6 @@ struct DeepQueue {
                              // the accumulation that reads it)
 };
 
-// Hot-first dealing: the reference's max-depth paths (rays trapped in the glass
-// spheres by its refract, raytracer.hxx:158-194) come from few tiles of a frame (config 3:
-// 12% of the 8x8 tiles hold every sample that passes kHotDepth segments). The render kernel
-// counts, per natural tile, the paths that reach kHotDepth (tile_stats); the accumulation of a
-// pass builds from those counts a plan for the next pass on its workspace: the hot tiles first,
-// then the others, each in natural order. A pass with a plan deals the hot tiles' samples
-// (sample-major over the hot tiles) from a ninth queue every wave serves first, then the rest
-// as before, so the long paths start at the beginning of the launch instead of anywhere in it
-// and the launch no longer ends with their ~64-iteration drain. Items map to the same (pixel,
-// sample) either way: the same bits. The hot region has its own 8 queues (one shared counter
-// serialised the whole grid's first grabs: config 3 3.45 vs 3.22 ms per frame).
-// plan words: [0] hot pixels (64 per hot tile; 0 = natural order), [1] tiles, [2..3] UDiv of
-// the hot pixel count, [4..5] UDiv of the other pixels' count, [6..7] 0, then perm[tiles]:
-// enumeration tile -> natural tile.
-constexpr uint32_t kPlanHeader = 8;
-constexpr uint32_t kHotDepth = 8;
-
 struct KParams {
     FrameConsts fc;
     // camera basis (rt_camera)
@@ -122,11 +105,6 @@ struct KParams {
     DeepQueue deep;
     uint32_t deep_depth;     // 0: no split (and always 0 in the deep launch)
     uint32_t deep_mode;      // the deep launch: the split depth (its paths resume there); 0 otherwise
-    // hot-first dealing: the plan of this pass (nullptr = natural order; guided dealing only)
-    // and the per-tile counters of paths reaching kHotDepth (nullptr = not counted)
-    const uint32_t *plan;
-    uint32_t *tile_stats;
-    uint32_t hot_sample_mask;  // samples of the pass counted: those with (sample & mask) == 0
 };
 
 struct KAccum {
@@ -157,11 +135,6 @@ struct KAccum {
     // flags; part 0 (unsplit pass): every pixel
     uint8_t *deep_px;
     uint32_t part;
-    // hot-first dealing: one extra workgroup builds the next plan of this workspace from the
-    // tile counters (and decays them); nullptr = none
-    uint32_t *plan_out;
-    uint32_t *tile_stats;
-    uint32_t n_tiles;        // tiles of this pass's layout (tiled_rows * W / 64)
 };
 
 // RT_FLAG_CUDA_COMPAT: the semantics of the reference's CUDA variant (src/CUDA/cuda_impl.cu),
@@ -198,7 +171,6 @@ struct KWave {
 constexpr uint32_t kQueueStride = 64;
 constexpr uint32_t kDeepDeal = 16;   // word of queue q's line (the deep launch deals while the queue counter is idle)
 constexpr uint32_t kDeepCount = 32;  // word of queue q's line, in its second 128-B half
-constexpr uint32_t kHotDeal = 48;    // word of queue q's line: hot queue q's ticket counter
 
 // V_STATS_LDS diagnostics buffer: 16 counters, then {start, exit, iterations, hw id | refills}
 // per wave

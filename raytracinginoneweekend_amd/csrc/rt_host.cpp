@@ -171,26 +171,6 @@ uint32_t tail_pct()
     return v <= 100 ? static_cast<uint32_t>(v) : 8u;
 }
 
-// Hot-first dealing (rt_device.h KParams::plan), RT_HOT_FIRST=1 turns it on.
-// RT_HOT_SPLIT=1 keeps the deep-path split in passes that have a plan (default: no split there,
-// the long paths already start at the beginning of the launch).
-bool hot_first_env()
-{
-    const char *e = std::getenv("RT_HOT_FIRST");
-    return e && e[0] == '1';
-}
-uint32_t hot_sample_mask_env()  // RT_HOT_SAMPLE_SHIFT=s: count 1 in 2^s samples (A/B)
-{
-    const char *e = std::getenv("RT_HOT_SAMPLE_SHIFT");
-    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 0ul;
-    return (1u << std::min<unsigned long>(v, 8ul)) - 1u;
-}
-bool hot_split_env()
-{
-    const char *e = std::getenv("RT_HOT_SPLIT");
-    return e && e[0] == '1';
-}
-
 } // namespace
 
 struct rt_scene {
@@ -224,15 +204,6 @@ struct rt_scene {
     static constexpr size_t kDeepOffKeys = 8;
     static constexpr uint64_t kDeepOffCalls = 256;
     std::vector<std::pair<unsigned long long, uint64_t>> deep_off;
-    // hot-first dealing (rt_device.h KParams::plan): per workspace the plan its last
-    // accumulation built and the layout it was built for (0 = none), and the per-tile counters
-    // of paths reaching kHotDepth of the layout stats_key
-    uint32_t *plan[kMaxWs] = {};
-    size_t plan_bytes[kMaxWs] = {};
-    unsigned long long plan_key[kMaxWs] = {};
-    uint32_t *tile_stats = nullptr;
-    size_t stats_bytes = 0;
-    unsigned long long stats_key = 0;
     void *wq = nullptr;  // RT_FLAG_WAVEFRONT: two ray queues and their counters
     size_t wq_bytes = 0;
     int occ_wave[2] = {-1, -1};  // wave_bounce_kernel blocks per CU [culled], -1 = unknown
@@ -910,9 +881,6 @@ int rt_scene_destroy(rt_scene *sc)
         if (p) (void)hipFree(p);
     for (void *p : sc->deep)
         if (p) (void)hipFree(p);
-    for (uint32_t *p : sc->plan)
-        if (p) (void)hipFree(p);
-    if (sc->tile_stats) (void)hipFree(sc->tile_stats);
     if (sc->deep_over) (void)hipHostFree(sc->deep_over);
     (void)hipSetDevice(prev);
     delete sc;
@@ -1247,32 +1215,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         wgrid = ow * sc->cu_count;
     }
 
-    // hot-first dealing: guided dealing of the megakernel only; the layout key names the camera,
-    // depth limit and pixel layout the tile counters and plans belong to
-    const bool hot = hot_first_env() && !wave && guided_l2b(64) < 0.f && n_pixels >= 64;
-    unsigned long long layout = 0;
-    uint32_t n_tiles = 0;
-    if (hot) {
-        rt::KParams lk = k;
-        lk.sample_begin = 0;
-        fill_frame_consts(lk);
-        n_tiles = static_cast<uint32_t>(static_cast<uint64_t>(lk.tiled_rows) * P.width / 64u);
-        const uint64_t words[] = {deep_key, P.width, P.height, lk.row_offset, lk.row_stride, lk.n_pixels, lk.tile_lw,
-                                  lk.tiled_rows};
-        layout = 1469598103934665603ull;
-        for (uint64_t w : words)
-            for (int b = 0; b < 8; ++b) layout = (layout ^ ((w >> (8 * b)) & 0xffu)) * 1099511628211ull;
-        layout |= 1ull;  // never 0 (= no plan)
-        if (n_tiles == 0) layout = 0;
-    }
-    if (layout) {
-        void *had = sc->tile_stats;
-        if (int rc = ensure((void **)&sc->tile_stats, &sc->stats_bytes, static_cast<size_t>(n_tiles) * 4u); rc) return rc;
-        if (sc->tile_stats != had || sc->stats_key != layout) {  // new memory or another layout: start over
-            RT_HIP(hipMemsetAsync(sc->tile_stats, 0, static_cast<size_t>(n_tiles) * 4u, st));
-            sc->stats_key = layout;
-        }
-    }
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
@@ -1310,16 +1252,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u);
-        // the plan this workspace's last accumulation built, if it was for this layout
-        k.plan = layout && sc->plan_key[wb] == layout ? sc->plan[wb] : nullptr;
-        k.tile_stats = layout ? sc->tile_stats : nullptr;
-        k.hot_sample_mask = hot_sample_mask_env();
-        if (layout) {  // this pass's accumulation builds the workspace's next plan
-            void *had = sc->plan[wb];
-            if (int rc = ensure((void **)&sc->plan[wb], &sc->plan_bytes[wb], (rt::kPlanHeader + 2u * static_cast<size_t>(n_tiles)) * 4u); rc)
-                return rc;
-            if (sc->plan[wb] != had) k.plan = nullptr;
-        }
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
         k.deep_depth = 0;
         k.deep_mode = 0;
@@ -1327,8 +1259,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         // culled scenes only: with a handful of spheres (the simple scene, brute force) a deep
         // segment is cheap and the deep launch's overhead outweighs the drain it saves
         // (config 2: 0.98-1.00 vs 0.98-0.99 ms per frame)
-        if (deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth && k.n_items >= deep_min_items &&
-            (!k.plan || hot_split_env())) {
+        if (deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth && k.n_items >= deep_min_items) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
             const size_t px_bytes = (n_pixels + 255u) & ~static_cast<size_t>(255u);
             void *had = sc->deep[wb];
@@ -1384,8 +1315,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 rt::KParams kd = k;
                 kd.deep_mode = k.deep_depth;
                 kd.deep_depth = 0;
-                kd.plan = nullptr;       // the deep launch deals queued paths
-                kd.tile_stats = nullptr;  // its paths were counted in the main launch
                 // the deep paths bounce inside glass spheres, inside the box over all clusters:
                 // the level-3 gate only costs there (alike within box noise, fewer box tests;
                 // same bits)
@@ -1418,12 +1347,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         a.row_stride = k.row_stride;
         a.full_frame = k.full_frame;
         if (pipe && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
-        if (layout) {
-            a.plan_out = sc->plan[wb];
-            a.tile_stats = sc->tile_stats;
-            a.n_tiles = n_tiles;
-            sc->plan_key[wb] = layout;  // valid for the next render on this workspace (it waits for this accumulation)
-        }
         a.queue_reset = k.queue_ctr;
         a.queue_words = 8 * rt::kQueueStride;
         if (k.deep_depth) {
@@ -1437,7 +1360,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             // the counters) after it. In a frame stream the other frames' work fills that time,
             // and the extra launch per pass measured ~1% slower there.
             rt::KAccum a1 = a;
-            a1.plan_out = nullptr;  // the plan is built by the last part
             a1.seg_from = a1.seg_to = nullptr;
             a1.queue_reset = nullptr;
             a1.deep_over = nullptr;

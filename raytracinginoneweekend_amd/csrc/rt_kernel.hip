@@ -251,6 +251,23 @@ struct Hit {  // the closest candidate so far as hit_key(t, original index); ~0 
     __device__ uint32_t id() const { return (uint32_t)key; }
 };
 constexpr uint64_t kNoHit = 0x7f7fffffffffffffull;  // t = kMAX, index = none
+// kNoHit made in VGPRs where it is used: left to itself the allocator keeps the constant in a
+// VGPR pair for the whole kernel, and at 7 waves per SIMD (72 VGPRs) spills it to scratch
+__device__ __forceinline__ uint64_t no_hit()
+{
+    uint32_t lo = 0xffffffffu, hi = 0x7f7fffffu;
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    return ((uint64_t)hi << 32) | lo;
+}
+// this lane's slot of a per-thread LDS array: the wave's first slot (a scalar) plus the lane
+// id, recomputed at each use (keeping threadIdx.x * 16 live across the loop costs a VGPR,
+// which at 7 waves per SIMD is spilled to scratch)
+__device__ __forceinline__ uint32_t thread_slot(uint32_t wave_base)
+{
+    uint32_t l;  // the lane id, formed here (the builtins' result is hoisted and kept live)
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return wave_base + l;
+}
 
 // Work counters of one wave (wave-uniform, scalar registers): segments traced and the
 // lane-level ray-sphere and cluster-box tests executed, summed from ballots in uniform control
@@ -586,14 +603,14 @@ __device__ __forceinline__ void cluster_members7(bool req, uint64_t M, uint32_t 
     }
 }
 
-template <bool FAST, int CULL, bool STATS, bool COUNT>
-__device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__restrict__ geo,
+template <bool FAST, int CULL, bool STATS, bool COUNT, class KP>
+__device__ __forceinline__ Hit closest_hit(const KP &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
                                            f3 d, const RayDiv &rd, Dbg &dbg, WaveTally<COUNT> &wt, bool active,
                                            uint64_t am, TransposeLds *tw)
 {
     // active: this lane traces a segment; am: the wave's mask of such lanes
-    Hit h{kNoHit};
+    Hit h{no_hit()};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
     if (CULL) {
         // 1/x with its magnitude clamped to 1e30 (one med3; |x| < 1e-30 behaves as 1e-30 of
@@ -645,44 +662,6 @@ __device__ __forceinline__ Hit closest_hit(const KParams &p, const float4 *__res
     return h;
 }
 
-// ---- hot-first dealing (rt_device.h KParams::plan) ----------------------------------------
-// a wave-uniform word of the plan (device memory written by the previous accumulation)
-__device__ __forceinline__ uint32_t plan_word(const uint32_t *plan, uint32_t i)
-{
-    return __builtin_amdgcn_readfirstlane(plan[i]);
-}
-// 64-item blocks of the hot region of a pass of ns samples: hot pixels (a multiple of 64) x ns
-__device__ __forceinline__ uint32_t plan_hot_blocks(const uint32_t *plan, uint32_t ns)
-{
-    return (plan_word(plan, 0) >> 6) * ns;
-}
-// item I of a pass of ns samples -> (natural pixel enumeration index, sample of the pass ls).
-// Without a plan (or with no hot tile): I = ls * n_pixels + pixel. With one: the hot region's
-// items first, sample-major over the hot pixels, then the others' items, sample-major over the
-// rest; enumeration pixel e is tile perm[e / 64] of the natural order (the untiled remainder
-// rows keep their place). Every (pixel, sample) is reached by exactly one item either way.
-template <class FC>
-__device__ __forceinline__ uint32_t item_pixel(const uint32_t *plan, const FC &fc, uint32_t I, uint32_t ns, uint32_t &ls)
-{
-    const uint32_t nh = plan ? plan_word(plan, 0) : 0u;
-    if (!nh) {
-        ls = udiv(I, fc.div_n_pixels.m, fc.div_n_pixels.l);
-        return I - ls * fc.n_pixels;
-    }
-    const uint32_t n_hot_items = nh * ns;
-    uint32_t e;
-    if (I < n_hot_items) {
-        ls = udiv(I, plan_word(plan, 2), plan_word(plan, 3));
-        e = I - ls * nh;
-    } else {
-        const uint32_t J = I - n_hot_items, nc = fc.n_pixels - nh;
-        ls = udiv(J, plan_word(plan, 4), plan_word(plan, 5));
-        e = nh + (J - ls * nc);
-    }
-    const uint32_t n_tiles = plan_word(plan, 1);
-    return (e >> 6) < n_tiles ? (plan[kPlanHeader + (e >> 6)] << 6) | (e & 63u) : e;
-}
-
 // ---- the megakernel ----------------------------------------------------------------------
 // p[i] read from global memory, named as such (a float4 load from address space 1)
 __device__ __forceinline__ float4 gld4(const float4 *p, uint32_t i)
@@ -696,8 +675,11 @@ __device__ __forceinline__ float4 gld4(const float4 *p, uint32_t i)
 // Structure 7 (the default) is held to 6 waves per SIMD: unhinted it takes 83 VGPRs (5 waves);
 // hinted, the allocator keeps 79 and parks one 12-byte constant that only the metal-absorption
 // path reloads (measured: 5.03-5.06 ms vs 5.19-5.24 per config-3 launch).
+#ifndef RT_CULL7_WAVES
+#define RT_CULL7_WAVES 7
+#endif
 template <int V, int CULL, bool STATS>
-constexpr int kMinWaves = (CULL == 7 && !STATS) ? 6 : RT_MIN_WAVES_PER_SIMD;
+constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_PER_SIMD;
 template <int V, int CULL, bool STATS, bool COUNT>
 __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kernel(const KParams p)
 {
@@ -721,6 +703,8 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     const fc_ptr_t fc_base =
         (fc_ptr_t)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() +
                    offsetof(KParams, fc));
+    typedef const __attribute__((address_space(4))) KParams *kp_ptr_t;
+    const kp_ptr_t kp_base = (kp_ptr_t)__builtin_amdgcn_kernarg_segment_ptr();
     const float4 *geo = blob;
     const uint32_t *sidx = reinterpret_cast<const uint32_t *>(blob + p.n_geo);
     const float4 *clus = blob + p.clus_offset;
@@ -733,11 +717,10 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         tw = &s_tw[threadIdx.x >> 6];
     }
     __shared__ float4 lds_pn[256];  // per lane: a pending metal scatter's normal and roughness
+    const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
-    // wave-uniform cursor over the item space (the deep launch: over the queued paths); with a
-    // hot-first plan every wave serves the 8 hot queues first (hotq), then the 8 others
+    // wave-uniform cursor over the item space (the deep launch: over the queued paths)
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
-    bool hotq = p.plan != nullptr;
     uint32_t cnext = 0, cend = 0;
     bool exhausted = false;
     bool deep_full = false;  // this wave's deep-queue region is full: no more splits
@@ -795,6 +778,12 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
 #endif
         fc_ptr_t fc = fc_base;
         asm volatile("" : "+s"(fc));
+        // the kernel parameters, re-read from the kernarg segment each iteration through an
+        // opaque pointer: their uses (the deep split, the shading records, the refill) then
+        // hold no SGPRs across the loop (31 SGPRs were spilled to VGPR lanes otherwise)
+        kp_ptr_t kpp = kp_base;
+        asm volatile("" : "+s"(kpp));
+        const __attribute__((address_space(4))) KParams &P = *kpp;
         // ---- refill items for idle lanes and start their samples -------------------
         uint64_t need = ballot(!alive);
         bool fresh = false;
@@ -803,72 +792,60 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             RT_EV(EV_REFILL_TRIP);
             if (cnext >= cend) {
                 uint32_t c = 0;
-                if (p.deep_mode) {
+                if (P.deep_mode) {
                     // the deep launch: 64 queued paths per grab from region q, then the next
                     // region (a wave starts on its workgroup's region)
-                    if (lane == 0) c = atomicAdd(p.deep.ctr + q * kQueueStride + kDeepDeal, 1u);
+                    if (lane == 0) c = atomicAdd(P.deep.ctr + q * kQueueStride + kDeepDeal, 1u);
                     c = __builtin_amdgcn_readfirstlane(c);
-                    const uint32_t nq = min(p.deep.ctr[q * kQueueStride + kDeepCount], p.deep.rcap);
+                    const uint32_t nq = min(P.deep.ctr[q * kQueueStride + kDeepCount], P.deep.rcap);
                     if (c >= (nq + 63u) / 64u) {
                         q = (q + 1u) & 7u;
                         if (++q_tried == 8u) exhausted = true;
                         continue;
                     }
-                    cnext = q * p.deep.rcap + 64u * c;
-                    cend = q * p.deep.rcap + min(64u * c + 64u, nq);
+                    cnext = q * P.deep.rcap + 64u * c;
+                    cend = q * P.deep.rcap + min(64u * c + 64u, nq);
                 } else {
-                if (lane == 0) c = atomicAdd(p.queue_ctr + q * kQueueStride + (hotq ? kHotDeal : 0u), 1u);
+                if (lane == 0) c = atomicAdd(P.queue_ctr + q * kQueueStride, 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
-                if (p.guided_l2b < 0.f) {
+                if (P.guided_l2b < 0.f) {
                     // guided: queue q owns blocks [qb0, qb1) of 64 items; ticket c takes blocks
                     // [S(c), S(c+1)), S(t) = min(B, floor(B (1 - beta^t)) + 2t): chunks shrink
                     // geometrically from ~B / (K waves per queue) to 2 blocks, so a queue is
                     // served by few atomics and its last chunks are small. S is the same
                     // function for every wave, so consecutive tickets tile the range; the 2t
                     // term keeps it increasing even if exp2 or the float product is off by an
-                    // ulp (one block at most). With a plan, the first hot_b blocks (the hot
-                    // tiles' samples) are shared by 8 hot queues that every wave serves first,
-                    // and the 8 queues share the rest.
-                    const uint32_t hot_b = p.plan ? plan_hot_blocks(p.plan, p.sample_end - p.sample_begin) : 0u;
-                    const uint32_t nb = hotq ? hot_b : p.n_blocks - hot_b;
-                    const uint32_t qb0 = (hotq ? 0u : hot_b) + (uint32_t)(((uint64_t)nb * q) >> 3);
-                    const uint32_t B = (uint32_t)(((uint64_t)nb * (q + 1u)) >> 3) - (uint32_t)(((uint64_t)nb * q) >> 3);
+                    // ulp (one block at most).
+                    const uint32_t qb0 = (uint32_t)(((uint64_t)P.n_blocks * q) >> 3);
+                    const uint32_t B = (uint32_t)(((uint64_t)P.n_blocks * (q + 1u)) >> 3) - qb0;
                     auto S = [&](uint32_t t) -> uint32_t {
-                        const float x = t ? exp2f((float)t * p.guided_l2b) : 1.f;
+                        const float x = t ? exp2f((float)t * P.guided_l2b) : 1.f;
                         const uint64_t g = (uint64_t)floorf((float)B * (1.f - x)) + 2ull * t;
                         return g < B ? (uint32_t)g : B;
                     };
                     const uint32_t s0 = S(c);
                     if (s0 >= B) {
                         q = (q + 1u) & 7u;
-                        if (++q_tried == 8u) {
-                            if (hotq) {  // every hot queue is dry: the others, from the wave's own
-                                hotq = false;
-                                q_tried = 0;
-                                q = blockIdx.x & 7u;
-                            } else {
-                                exhausted = true;
-                            }
-                        }
+                        if (++q_tried == 8u) exhausted = true;
                         continue;
                     }
                     cnext = 64u * (qb0 + s0);
-                    cend = min(64u * (qb0 + S(c + 1u)), p.n_items);
+                    cend = min(64u * (qb0 + S(c + 1u)), P.n_items);
                 } else {
                 const uint64_t chunk = (uint64_t)q + 8ull * c;
-                if (chunk >= p.n_chunks) {
+                if (chunk >= P.n_chunks) {
                     q = (q + 1u) & 7u;
                     if (++q_tried == 8u) exhausted = true;
                     continue;
                 }
                 // big chunks first, then 64-item chunks for the end of the launch: a wave
                 // then holds at most 64 undealt items when the queues run dry
-                if (chunk < p.n_big_chunks) {
-                    cnext = (uint32_t)chunk * p.chunk_items;
-                    cend = cnext + p.chunk_items;
+                if (chunk < P.n_big_chunks) {
+                    cnext = (uint32_t)chunk * P.chunk_items;
+                    cend = cnext + P.chunk_items;
                 } else {
-                    cnext = p.n_big_chunks * p.chunk_items + ((uint32_t)chunk - p.n_big_chunks) * 64u;
-                    cend = min(cnext + 64u, p.n_items);
+                    cnext = P.n_big_chunks * P.chunk_items + ((uint32_t)chunk - P.n_big_chunks) * 64u;
+                    cend = min(cnext + 64u, P.n_items);
                 }
                 }
                 }
@@ -878,22 +855,23 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (!alive && rank < avail) {
                 const uint32_t I = cnext + rank;
-                if (p.deep_mode) {
+                if (P.deep_mode) {
                     // a queued path resumes where the main launch left it: the ray of its next
                     // segment, attenuation, data stream and segment count; ls = 0 and pix = the
                     // slot index address the same slot
-                    const uint32_t cap = 8u * p.deep.rcap;
-                    const float *f = p.deep.f;
+                    const uint32_t cap = 8u * P.deep.rcap;
+                    const float *f = P.deep.f;
                     o = mk(f[I], f[cap + I], f[2 * cap + I]);
                     d = mk(f[3 * cap + I], f[4 * cap + I], f[5 * cap + I]);
                     att = mk(f[6 * cap + I], f[7 * cap + I], f[8 * cap + I]);
-                    rng = p.deep.rng[I];
-                    pix = p.deep.slot[I];
+                    rng = P.deep.rng[I];
+                    pix = P.deep.slot[I];
                     ls = 0;
-                    depth = p.deep_mode;
+                    depth = P.deep_mode;
                     alive = true;
                 } else {
-                    pix = item_pixel(p.plan, *fc, I, p.sample_end - p.sample_begin, ls);
+                    ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
+                    pix = I - ls * fc->n_pixels;
                     alive = fresh = true;
                 }
             }
@@ -980,17 +958,21 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                 if (!pend_metal) {
                     d = (d + r) - o;                       // lambert :135, d held p + n, o = p
                 } else {
-                    const float4 pn = lds_pn[threadIdx.x];
+                    const float4 pn = lds_pn[thread_slot(wave_base)];
                     const f3 nd = d + r * pn.w;            // metal :147, d held reflect(unit(d), n)
                     if (dot(nd, mk(pn.x, pn.y, pn.z)) > 0.f) {
                         d = nd;
                     } else {                               // absorbed: main.cxx:68, colour 0
                         RT_EV(EV_METAL_ABSORB);
                         alive = false;
-                        float *dst = p.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
-                        dst[0] = 0.f;
-                        dst[1] = 0.f;
-                        dst[2] = 0.f;
+                        float *dst = P.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
+                        // zeros made here (left to itself the allocator parks a zero triple in
+                        // scratch for this rare path)
+                        float z = 0.f;
+                        asm volatile("" : "+v"(z));
+                        dst[0] = z;
+                        dst[1] = z;
+                        dst[2] = z;
                     }
                 }
                 pend = false;
@@ -1012,35 +994,28 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         // Paths are appended to region blockIdx % 8 of the queue (8 counters on separate
         // lines, so the appends of the whole grid do not serialise on one address); a wave
         // that finds its region full stops splitting.
-        if (p.tile_stats) {  // hot-first dealing: count the paths that reach kHotDepth per tile
-            const bool hs = alive && !defer && depth == kHotDepth && (ls & p.hot_sample_mask) == 0u;
-            if (ballot(hs)) {
-                const uint32_t tiled_px = fc->tiled_rows * fc->W;
-                if (hs && pix < tiled_px) atomicAdd(p.tile_stats + (pix >> 6), 1u);
-            }
-        }
-        if (p.deep_depth && !deep_full) {
-            const bool dv = alive && !defer && depth == p.deep_depth;
+        if (P.deep_depth && !deep_full) {
+            const bool dv = alive && !defer && depth == P.deep_depth;
             const uint64_t m = ballot(dv);
             if (m) {
                 const uint32_t r = blockIdx.x & 7u;
                 const uint32_t nm = (uint32_t)__popcll(m);
                 uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(p.deep.ctr + r * kQueueStride + kDeepCount, nm);
+                if (lane == 0) base = atomicAdd(P.deep.ctr + r * kQueueStride + kDeepCount, nm);
                 base = __builtin_amdgcn_readfirstlane(base);
-                if (base + nm >= p.deep.rcap) deep_full = true;
+                if (base + nm >= P.deep.rcap) deep_full = true;
                 uint32_t j = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                if (dv && j < p.deep.rcap) {
-                    const uint32_t cap = 8u * p.deep.rcap;
-                    j += r * p.deep.rcap;
-                    float *f = p.deep.f;
+                if (dv && j < P.deep.rcap) {
+                    const uint32_t cap = 8u * P.deep.rcap;
+                    j += r * P.deep.rcap;
+                    float *f = P.deep.f;
                     f[j] = o.x; f[cap + j] = o.y; f[2 * cap + j] = o.z;
                     f[3 * cap + j] = d.x; f[4 * cap + j] = d.y; f[5 * cap + j] = d.z;
                     f[6 * cap + j] = att.x; f[7 * cap + j] = att.y; f[8 * cap + j] = att.z;
-                    p.deep.rng[j] = rng;
-                    p.deep.slot[j] = ls * fc->n_pixels + pix;
-                    p.deep.px[pix] = 1;
+                    P.deep.rng[j] = rng;
+                    P.deep.slot[j] = ls * fc->n_pixels + pix;
+                    P.deep.px[pix] = 1;
                     alive = false;
                 }
             }
@@ -1065,24 +1040,24 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         }
 
         // ---- closest hit of one segment for every live lane -----------------------------
-        const bool seg = alive && !defer && depth < p.max_depth;  // depth check: main.cxx:74
+        const bool seg = alive && !defer && depth < P.max_depth;  // depth check: main.cxx:74
         // |d|^2 (raytracer.hxx:56) and its refined reciprocal for this segment's roots; the sky
         // below reuses both (unit_direction's length is sqrt of the same sum)
         const float a = d.x * d.x + d.y * d.y + d.z * d.z;
         const uint64_t segm = ballot(seg);
-        const RayDiv rd = ray_div(a, segm, p.fast_roots);
+        const RayDiv rd = ray_div(a, segm, P.fast_roots);
         Hit h{kNoHit};
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
-            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, tw);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, tw);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
-            h = closest_hit<FAST, CULL, STATS, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr);
         }
         stamp(2);
         {
             const uint32_t ns = lanes(seg);  // segments of this iteration (main.cxx:74 passed)
             wt.add_seg(ns);
-            wt.add_sph((uint64_t)ns * p.n_always);
+            wt.add_sph((uint64_t)ns * P.n_always);
         }
 
         // ---- shading: the hit of every live lane -----------------------------------------
@@ -1113,7 +1088,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     const f3 bg = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
                     col = bg * att;
                     done = true;
-                } else if (depth >= p.max_depth) {
+                } else if (depth >= P.max_depth) {
                     // main.cxx:65-74: a scattered ray would not be traced and an absorbed one
                     // returns 0 too; this sample's streams are not drawn from again
                     done = true;
@@ -1121,28 +1096,28 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     RT_EV(EV_HIT);
                     float4 sf, md;
                     uint32_t kind;
-                    if (V != V_EXACT_SCALAR && p.shade_lds) {
-                        const float4 *shade = blob + p.shade_offset;
+                    if (V != V_EXACT_SCALAR && P.shade_lds) {
+                        const float4 *shade = blob + P.shade_offset;
                         sf = shade[2 * ib];
                         md = shade[2 * ib + 1];
-                        kind = reinterpret_cast<const uint8_t *>(shade + 2 * p.n_spheres)[ib];
+                        kind = reinterpret_cast<const uint8_t *>(shade + 2 * P.n_spheres)[ib];
                         asm volatile("");  // keeps the LDS and global loads apart (no sinking)
                     } else {
                         // global memory, named as such: the two branches' loads would otherwise be
                         // merged into flat loads through a selected pointer
-                        const float4 *shade = p.blob + p.shade_offset;
+                        const float4 *shade = P.blob + P.shade_offset;
                         sf = gld4(shade, 2 * ib);
                         md = gld4(shade, 2 * ib + 1);
-                        kind = ((const __attribute__((address_space(1))) uint8_t *)(shade + 2 * p.n_spheres))[ib];
+                        kind = ((const __attribute__((address_space(1))) uint8_t *)(shade + 2 * P.n_spheres))[ib];
                     }
                     const f3 ctr = mk(sf.x, sf.y, sf.z);
                     const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
                     // raytracer.hxx:71. With the scene in the short-form range (|r| in [2^-40, 2^19],
-                    // p.fast_roots) the division by r takes the short form unless a lane's offset has
+                    // P.fast_roots) the division by r takes the short form unless a lane's offset has
                     // a component below 2^-100 (zero included).
                     const f3 dv = hp - ctr;
                     f3 hn;
-                    if (p.fast_roots && all_lanes_min_abs_ok(dv)) hn = div3_short(dv, sf.w);
+                    if (P.fast_roots && all_lanes_min_abs_ok(dv)) hn = div3_short(dv, sf.w);
                     else hn = dv / sf.w;
                     att = att * mk(md.x, md.y, md.z);           // main.cxx:65 (unused if absorbed)
                     // raytracer.hxx:120-199
@@ -1166,19 +1141,19 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                         const f3 rf = reflect(ud, hn);
                         if (kind == 1u) {                       // metal, :143-156
                             d = rf;                             // + rius * roughness next iteration
-                            lds_pn[threadIdx.x] = make_float4(hn.x, hn.y, hn.z, md.w);
+                            lds_pn[thread_slot(wave_base)] = make_float4(hn.x, hn.y, hn.z, md.w);
                             pend = true;
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
                             RT_EV(EV_DIELECTRIC);
                             // {1 / ior, x(ior), x(1 / ior)} of this sphere, x(r) = (1 - r) / (1 + r)
-                            const uint32_t di = p.shade_offset + 2 * p.n_spheres + (p.n_spheres + 15u) / 16u + ib;
+                            const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
                             float4 dcs;
-                            if (V != V_EXACT_SCALAR && p.shade_lds) {
+                            if (V != V_EXACT_SCALAR && P.shade_lds) {
                                 dcs = blob[di];
                                 asm volatile("");  // no merged (flat) load, as above
                             } else {
-                                dcs = gld4(p.blob, di);
+                                dcs = gld4(P.blob, di);
                             }
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w, xs = dcs.y;
@@ -1204,7 +1179,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                 // the sample's colour goes to its slot; accumulate_kernel forms the reference's
                 // blocked sum over the slots (main.cxx:205)
                 alive = false;
-                float *dst = p.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
+                float *dst = P.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
                 dst[0] = col.x;
                 dst[1] = col.y;
                 dst[2] = col.z;
@@ -1433,80 +1408,6 @@ __global__ __launch_bounds__(256) void compat_kernel(const KCompat p)
     }
 }
 
-// ---- the next hot-first plan (one workgroup of accumulate_kernel) ----------------------------
-// From the tile counters (paths that reached kHotDepth, counted by the renders of this scene
-// and layout; other renders may add to them meanwhile, which only changes the choice): a tile
-// is hot if its counter is non-zero. The flags are snapshotted first (words [kPlanHeader + T,
-// kPlanHeader + 2T) of the plan), so the permutation is built from one consistent choice: hot
-// tiles first, then the others, each in natural order. More than half the tiles hot (long
-// paths everywhere, e.g. the corrected camera): natural order. The counters are halved
-// (rounding down), so a tile stays hot while its paths keep reaching kHotDepth.
-__device__ __forceinline__ UDiv udiv_magic(uint32_t d)  // rt_host.cpp make_udiv
-{
-    UDiv r{0u, 0u};
-    if (d <= 1u) return r;
-    const uint32_t l = 32u - (uint32_t)__clz(d - 1u);
-    r.l = l;
-    r.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1u);
-    return r;
-}
-__device__ void build_plan(const KAccum &k)
-{
-    __shared__ uint32_t s_wave[4];
-    const uint32_t T = k.n_tiles, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    uint32_t *flag = k.plan_out + kPlanHeader + T;
-    // block-wide exclusive prefix of v (256 threads: 4 waves) and the total
-    auto block_scan = [&](uint32_t v, uint32_t &total) -> uint32_t {
-        uint32_t x = v;  // inclusive scan within the wave
-        for (uint32_t off = 1; off < 64u; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off);
-            if (lane >= off) x += y;
-        }
-        if (lane == 63u) s_wave[wv] = x;
-        __syncthreads();
-        uint32_t base = 0;
-        for (uint32_t w = 0; w < wv; ++w) base += s_wave[w];
-        total = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-        __syncthreads();
-        return base + x - v;
-    };
-    // 1. snapshot the flags (and halve the counters), count the hot tiles
-    uint32_t H = 0;
-    for (uint32_t t0 = 0; t0 < T; t0 += 256u) {
-        const uint32_t t = t0 + tid;
-        uint32_t f = 0;
-        if (t < T) {
-            const uint32_t c = k.tile_stats[t];
-            f = c != 0u;
-            flag[t] = f;
-            if (c) atomicSub(k.tile_stats + t, c - (c >> 1));
-        }
-        uint32_t tot;
-        block_scan(f, tot);
-        H += tot;
-    }
-    if (2u * H > T) H = 0;  // long paths everywhere: natural order
-    // 2. the permutation: position of hot tile t = hot tiles before it; of cold tile t = H + cold before it
-    uint32_t hot_before = 0;
-    for (uint32_t t0 = 0; t0 < T; t0 += 256u) {
-        const uint32_t t = t0 + tid;
-        const uint32_t f = (t < T && H) ? flag[t] : 0u;
-        uint32_t tot;
-        const uint32_t hb = hot_before + block_scan(f, tot);
-        if (t < T) k.plan_out[kPlanHeader + (f ? hb : H + (t - hb))] = t;
-        hot_before += tot;
-    }
-    if (tid == 0) {
-        const uint32_t nh = 64u * H;
-        const UDiv dh = udiv_magic(nh), dc = udiv_magic(k.n_pixels - nh);
-        k.plan_out[0] = nh;
-        k.plan_out[1] = T;
-        k.plan_out[2] = dh.m; k.plan_out[3] = dh.l;
-        k.plan_out[4] = dc.m; k.plan_out[5] = dc.l;
-        k.plan_out[6] = 0u; k.plan_out[7] = 0u;
-    }
-}
-
 // ---- ordered accumulation of the slots, average, optional gamma/u8 --------------------
 __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
 {
@@ -1524,10 +1425,6 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
                 *k.deep_over = k.deep_key;
             k.queue_reset[w] = 0u;
         }
-    if (k.plan_out && blockIdx.x == gridDim.x - 1u) {  // the extra workgroup: the next plan
-        build_plan(k);
-        return;
-    }
     if (i >= k.n_pixels) return;
     // split passes (KAccum::part): 1 = pixels without deep samples, 2 = the others, 3 = all
     // pixels in one part; 2 and 3 clear the flags for the workspace's next pass
@@ -1648,6 +1545,8 @@ __global__ __launch_bounds__(256, 6) void wave_bounce_kernel(const KWave w)
     for (uint32_t i = threadIdx.x; i < p.lds_units; i += blockDim.x) lds_blob[i] = p.blob[i];
     __syncthreads();
     const float4 *blob = lds_blob;
+    typedef const __attribute__((address_space(4))) KParams *kp_ptr_t;
+    const kp_ptr_t kp_base = (kp_ptr_t)__builtin_amdgcn_kernarg_segment_ptr();
     const float4 *geo = blob;
     const uint32_t *sidx = reinterpret_cast<const uint32_t *>(blob + p.n_geo);
     const float4 *clus = blob + p.clus_offset;
@@ -1885,7 +1784,7 @@ hipError_t occupancy_compat(int *blocks_per_cu)
 
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream)
 {
-    const uint32_t grid = (k.n_pixels + 255u) / 256u + (k.plan_out ? 1u : 0u);
+    const uint32_t grid = (k.n_pixels + 255u) / 256u;
     hipLaunchKernelGGL(accumulate_kernel, dim3(grid), dim3(256), 0, stream, k);
     return hipGetLastError();
 }

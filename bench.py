@@ -83,7 +83,7 @@ def parse():
                          "estimate one rank's frame time at N GPUs; not a bench line")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process, set before HIP starts (0: leave the environment, "
-                         "HIP's default 4): the library runs one render stream fewer than this, 2..4 "
+                         "HIP's default 4): the library runs one render stream fewer than this, 2..7 "
                          "(rt_host.cpp pipeline_env); the line records both values")
     ap.add_argument("--output", default="f32", choices=["f32", "rgb8"],
                     help="f32: the linear frame (12 B/pixel gathered); rgb8: gamma/u8 epilogue on every rank "
@@ -255,11 +255,11 @@ def pmc_fields(path, kernel, config):
 
 def frames_in_flight():
     """Render streams (RT_PIPELINE, rt_host.cpp pipeline_env: by default GPU_MAX_HW_QUEUES - 1,
-    within 2..4)."""
+    within 2..7)."""
     v = os.environ.get("RT_PIPELINE", "")
     if v:
-        return max(1, min(int(v), 4))
-    return max(2, min(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) - 1, 4))
+        return max(1, min(int(v), 8))
+    return max(2, min(env_int("GPU_MAX_HW_QUEUES", 4) - 1, 7))
 
 
 def cpu_info():

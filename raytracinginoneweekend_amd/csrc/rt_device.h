@@ -41,8 +41,8 @@ struct FrameConsts {
 };
 
 // The deep queue of one workspace (structure of arrays, 8 regions of rcap paths): f =
-// [9][8 rcap] floats {o.xyz, d.xyz, attenuation.xyz} of the next segment, the data-stream state
-// and the sample's slot index. Region r is appended to by workgroups r mod 8; its counters sit in
+// [9][8 rcap] floats {o.xyz, d.xyz, attenuation.xyz} of the next segment, the data-stream state,
+// the sample's slot index and the path's hint sphere (52 B per path). Region r is appended to by workgroups r mod 8; its counters sit in
 // the workspace's queue-counter block, line r: word kDeepCount = paths appended (may exceed
 // rcap: lanes past it keep their path), word kDeepDeal = the deep launch's dealing counter;
 // they are reset with the queue counters.
@@ -50,6 +50,7 @@ struct DeepQueue {
     float *f;
     uint64_t *rng;
     uint32_t *slot;
+    uint32_t *hid;           // the dielectric sphere the path last hit (its hint), ~0 = none
     uint32_t *ctr;           // the workspace's queue-counter block (8 x kQueueStride words)
     uint32_t rcap;
     uint8_t *px;             // [n_pixels] 1: some sample of the pixel went to the queue (cleared by
@@ -105,6 +106,7 @@ struct KParams {
     DeepQueue deep;
     uint32_t deep_depth;     // 0: no split (and always 0 in the deep launch)
     uint32_t deep_mode;      // the deep launch: the split depth (its paths resume there); 0 otherwise
+    uint32_t deep_prio;      // the deep launch's waves at the highest issue priority (s_setprio 3)
 };
 
 struct KAccum {

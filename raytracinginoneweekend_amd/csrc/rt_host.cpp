@@ -717,15 +717,29 @@ uint32_t deep_split_env()
 }
 // deep queue of a pass: 8 regions of 1/1024 of its samples each (at least 512): 0.8% of the
 // samples, where 0.2-0.3% reach the split depth on config 3; paths past a full region stay in the
-// main launch. Passes of fewer than RT_DEEP_MIN_ITEMS samples (default 2^25) are not split: the
-// deep launch is a serial tail of about max_depth - split iterations, which a small pass's own
-// drain does not outweigh (config 3's 8-way row share: 0.58-0.65 vs 0.52 ms per frame).
+// main launch. A pass of fewer than RT_DEEP_MIN_ITEMS samples (default 2^25) issued while no
+// other render runs (a lone frame) is not split: its deep launch would be a serial tail of
+// about max_depth - split iterations, which such a pass's own drain does not outweigh (config
+// 3's 8-way row share alone: 1.28-1.30 ms split vs 1.03-1.10). Passes issued while others run
+// (a frame stream) are split at any size: the unsplit drain costs issue (the 8-way share ran
+// 42% more VALU instructions per sample than the full frame) and the deep launches run beside
+// the other frames (8-way share, 7 streams: 0.50-0.51 ms per frame vs 0.58-0.59 unsplit).
 uint32_t deep_region_cap(uint32_t n_items)
 {
     const char *e = std::getenv("RT_DEEP_REGION_DIV");
     const unsigned long div = e && *e ? std::max(1ul, std::strtoul(e, nullptr, 10)) : 1024ul;
     return std::max<uint32_t>(512u, static_cast<uint32_t>(n_items / div));
 }
+// The deep launch's waves take the highest issue priority (RT_DEEP_PRIO=0 turns it off, A/B):
+// its paths are chains of ~56 dependent iterations, and beside other renders' waves each
+// iteration waits for the SIMD's other waves. Config 3's 8-way row share, split, 7 streams:
+// 0.513-0.515 ms vs 0.569-0.571 (profiles/r03/ab/deep_prio.txt); the full frame alike.
+uint32_t deep_prio_env()
+{
+    const char *e = std::getenv("RT_DEEP_PRIO");
+    return e && e[0] == '0' ? 0u : 1u;
+}
+
 // RT_DEEP_ROOT_BOX=1 keeps the level-3 box gate in the deep launch (A/B; default off)
 bool deep_root_box_env()
 {
@@ -773,9 +787,11 @@ uint32_t pipeline_env()
     if (!e || !*e) {
         const char *q = std::getenv("GPU_MAX_HW_QUEUES");
         const unsigned long hw = q && *q ? std::strtoul(q, nullptr, 10) : 4ul;
-        // default at most 4: 4 / 6 / 7 streams measure alike on config 3 and its 8-way row share
-        // (profiles/r02/ab/pipeline_streams_*.txt), and each stream holds two slot workspaces
-        return static_cast<uint32_t>(std::clamp<unsigned long>(hw > 1 ? hw - 1 : 1, 2, 4));
+        // at most 7: with row shares split (passes in flight) 7 streams beat 4 (config 3's 8-way
+        // share 0.50 vs 0.58 ms, 4-way 0.88 vs 0.95; the full frame 2.99-3.04 vs 3.06-3.08) and
+        // 8 (on 12 hardware queues) is slower again (profiles/r03/ab); each stream holds two
+        // slot workspaces
+        return static_cast<uint32_t>(std::clamp<unsigned long>(hw > 1 ? hw - 1 : 1, 2, 7));
     }
     const unsigned long v = std::strtoul(e, nullptr, 10);
     return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxBufs));
@@ -1259,11 +1275,11 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         // culled scenes only: with a handful of spheres (the simple scene, brute force) a deep
         // segment is cheap and the deep launch's overhead outweighs the drain it saves
         // (config 2: 0.98-1.00 vs 0.98-0.99 ms per frame)
-        if (deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth && k.n_items >= deep_min_items) {
+        if (deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth && (k.n_items >= deep_min_items || in_flight)) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
             const size_t px_bytes = (n_pixels + 255u) & ~static_cast<size_t>(255u);
             void *had = sc->deep[wb];
-            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], px_bytes + static_cast<size_t>(cap) * 48u); rc) return rc;
+            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], px_bytes + static_cast<size_t>(cap) * 52u); rc) return rc;
             if (sc->deep[wb] != had) sc->deep_clean[wb] = 0;  // new memory
             if (sc->deep_clean[wb] < px_bytes) {  // flags over bytes a queue may have used
                 RT_HIP(hipMemsetAsync(sc->deep[wb], 0, px_bytes, xst));
@@ -1275,6 +1291,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             k.deep.f = reinterpret_cast<float *>(base);
             k.deep.rng = reinterpret_cast<uint64_t *>(base + static_cast<size_t>(cap) * 36u);
             k.deep.slot = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 44u);
+            k.deep.hid = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 48u);
             k.deep.ctr = k.queue_ctr;
             k.deep.rcap = rcap;
             k.deep_depth = deep_split;
@@ -1319,6 +1336,12 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 // the level-3 gate only costs there (alike within box noise, fewer box tests;
                 // same bits)
                 kd.use_root = deep_root_box_env() ? k.use_root : 0u;
+                kd.deep_prio = deep_prio_env();
+                if (variant == rt::V_STATS_LDS && std::getenv("RT_DEBUG_DEEP_ONLY")) {
+                    // diagnostics: the counters and events of the deep launch alone
+                    RT_HIP(hipMemsetAsync(sc->dbg, 0, 16 * sizeof(unsigned long long), xst));
+                    RT_HIP(hipMemsetAsync(sc->dbg + rt::kDbgEvBase, 0, rt::kDbgEvents * sizeof(unsigned long long), xst));
+                }
                 RT_HIP(rt::launch_render(variant, cull_mode, kd, grid, xst));
             }
         }

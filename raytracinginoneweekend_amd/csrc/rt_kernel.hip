@@ -603,14 +603,58 @@ __device__ __forceinline__ void cluster_members7(bool req, uint64_t M, uint32_t 
     }
 }
 
+// The sphere a path last refracted into or reflected off inside (a dielectric hit), tested
+// first: a ray trapped in a small glass sphere (the reference's refract, raytracer.hxx:158-194,
+// keeps 0.17% of the samples bouncing up to max_depth, nearly all inside small dielectric
+// spheres) then starts the walk with t_best at that sphere's far wall, and the padded boxes of
+// every cluster its short segment does not reach are culled, where before the ground's or no
+// t_best let a wave's 64 paths request ~8 clusters per segment (deep launch, STATS events).
+// The candidate is the reference's (raytracer.hxx:55-90, the op sequence of test_block8 on
+// the sphere's geo entry {C, fl(r r)}), so the (t, index) minimum is unchanged when the walk
+// meets the sphere again. hint: this lane's last hit was a dielectric sphere, whose geo entry
+// and original index wait in the lane's LDS slots.
+template <bool FAST>
+__device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t id, f3 o, f3 d, const RayDiv &rd)
+{
+    const float a = rd.a;
+    const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;            // raytracer.hxx:55
+    float b, disc;
+    if (FAST) {
+        b = fmaf(ocx, d.x, fmaf(ocy, d.y, ocz * d.z));
+        const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -s.w)));
+        disc = fmaf(b, b, -(a * c));
+    } else {
+        b = ocx * d.x + ocy * d.y + ocz * d.z;                               // :57
+        const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;             // :58
+        disc = b * b - a * c;                                                // :60
+    }
+    const bool pos = hint && disc > 0.f;                                     // :62
+    const uint64_t posm = ballot(pos);
+    if (!posm) return no_hit();
+    const float dk = pos ? disc : -1.f;  // NaN candidate without a positive discriminant
+    float q;
+    float t = near_root(b, dk, rd, q);                                       // :63
+    const bool ok = in_range(t);
+    if (posm & ~ballot(ok)) {
+        const float t2 = far_root(b, q, rd);                                 // :76
+        t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
+    } else {
+        t = ok ? t : __builtin_nanf("");
+    }
+    const uint64_t kt = hit_key(t, id);
+    const uint64_t none = no_hit();
+    return kt < none ? kt : none;  // a NaN key (no candidate) orders above kNoHit: none then
+}
+
 template <bool FAST, int CULL, bool STATS, bool COUNT, class KP>
 __device__ __forceinline__ Hit closest_hit(const KP &p, const float4 *__restrict__ geo,
                                            const uint32_t *__restrict__ sidx, const float4 *__restrict__ clus, f3 o,
                                            f3 d, const RayDiv &rd, Dbg &dbg, WaveTally<COUNT> &wt, bool active,
-                                           uint64_t am, TransposeLds *tw)
+                                           uint64_t am, TransposeLds *tw, uint64_t key0)
 {
-    // active: this lane traces a segment; am: the wave's mask of such lanes
-    Hit h{no_hit()};
+    // active: this lane traces a segment; am: the wave's mask of such lanes; key0: a candidate
+    // already found for this segment (hint_candidate) or no_hit()
+    Hit h{key0};
     run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
     if (CULL) {
         // 1/x with its magnitude clamped to 1e30 (one med3; |x| < 1e-30 behaves as 1e-30 of
@@ -716,14 +760,20 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         __shared__ TransposeLds s_tw[4];
         tw = &s_tw[threadIdx.x >> 6];
     }
-    __shared__ float4 lds_pn[256];  // per lane: a pending metal scatter's normal and roughness
+    // per lane: a pending metal scatter's normal and roughness, or the geo entry {C, fl(r r)} of
+    // the dielectric sphere the lane's path last hit (hint_candidate; its original index in lds_hid)
+    __shared__ float4 lds_pn[256];
+    __shared__ uint32_t lds_hid[256];
     const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
+    // the deep launch's waves issue ahead of other launches' waves (KParams::deep_prio): each of
+    // its paths is a chain of ~56 dependent iterations, which beside other renders' waves on the
+    // same SIMD would take ~7x as long
+    if (p.deep_mode && p.deep_prio) __builtin_amdgcn_s_setprio(3);
     // wave-uniform cursor over the item space (the deep launch: over the queued paths)
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
     uint32_t cnext = 0, cend = 0;
     bool exhausted = false;
-    bool deep_full = false;  // this wave's deep-queue region is full: no more splits
 
     // lane state: the lane's item is one sample (pixel enumeration index, sample of the pass)
     bool alive = false;
@@ -738,6 +788,9 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     // a fresh sample whose lens draw did not finish within RT_REJECT_CAP attempts: its camera
     // stream state waits in (o.x, o.y) and its jittered (u, v) in (d.x, d.y) until it does
     bool pend_lens = false;
+    // lds_hid[lane] != ~0: the lane's last hit was a dielectric sphere, tested first next segment
+    // (hint_candidate); kept in LDS, not in a register (at 72 VGPRs one more value spills)
+    lds_hid[thread_slot(wave_base)] = ~0u;
     WaveTally<COUNT> wt;
     Dbg dbg{};
     uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0;
@@ -869,6 +922,13 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     ls = 0;
                     depth = P.deep_mode;
                     alive = true;
+                    // its hint sphere (hint_candidate): the geo entry from the shading record
+                    const uint32_t hid = P.deep.hid[I], sl = thread_slot(wave_base);
+                    if (hid != ~0u) {
+                        const float4 sf = gld4(P.blob + P.shade_offset, 2u * hid);
+                        lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);
+                    }
+                    lds_hid[sl] = hid;
                 } else {
                     ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
                     pix = I - ls * fc->n_pixels;
@@ -907,6 +967,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             vv = v + div_const(canonical(rng, inc_data), fH, rH, fh);
             att = mk(1.f, 1.f, 1.f);
             depth = 0;
+            lds_hid[thread_slot(wave_base)] = ~0u;
         }
         // ---- one rejection loop for the wave (raytracer.hxx:32-43) ------------------------
         // Fresh lanes draw the lens offset from their camera stream (camera.hxx:52); lanes
@@ -991,21 +1052,21 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         // glass spheres) then no longer hold this launch's waves for ~max_depth iterations after
         // the item queues run dry; the deep launch runs them with every lane busy. Each path
         // sees the same operations and draws in the same order: same bits.
-        // Paths are appended to region blockIdx % 8 of the queue (8 counters on separate
-        // lines, so the appends of the whole grid do not serialise on one address); a wave
-        // that finds its region full stops splitting.
-        if (P.deep_depth && !deep_full) {
+        // A path goes to region (its dielectric sphere's index) % 8 of the queue, or
+        // blockIdx % 8 if its last hit was not dielectric: the paths trapped in one sphere then
+        // share a region, and the deep launch's waves, which deal 64 paths at a time from one
+        // region, trace paths of the same few spheres, whose segments reach the same few
+        // clusters (8 counters on separate lines spread the appends). A path that finds its
+        // region full stays in this launch.
+        if (P.deep_depth) {
             const bool dv = alive && !defer && depth == P.deep_depth;
-            const uint64_t m = ballot(dv);
-            if (m) {
-                const uint32_t r = blockIdx.x & 7u;
-                const uint32_t nm = (uint32_t)__popcll(m);
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(P.deep.ctr + r * kQueueStride + kDeepCount, nm);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (base + nm >= P.deep.rcap) deep_full = true;
-                uint32_t j = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (ballot(dv)) {
+                uint32_t j = ~0u, r = 0;
+                if (dv) {
+                    const uint32_t hid = lds_hid[thread_slot(wave_base)];
+                    r = hid != ~0u ? (hid & 7u) : (blockIdx.x & 7u);
+                    j = atomicAdd(P.deep.ctr + r * kQueueStride + kDeepCount, 1u);
+                }
                 if (dv && j < P.deep.rcap) {
                     const uint32_t cap = 8u * P.deep.rcap;
                     j += r * P.deep.rcap;
@@ -1015,6 +1076,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     f[6 * cap + j] = att.x; f[7 * cap + j] = att.y; f[8 * cap + j] = att.z;
                     P.deep.rng[j] = rng;
                     P.deep.slot[j] = ls * fc->n_pixels + pix;
+                    P.deep.hid[j] = lds_hid[thread_slot(wave_base)];
                     P.deep.px[pix] = 1;
                     alive = false;
                 }
@@ -1048,10 +1110,14 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         const RayDiv rd = ray_div(a, segm, P.fast_roots);
         Hit h{kNoHit};
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
-            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, tw);
+            uint64_t key0 = no_hit();
+            const uint32_t sl = thread_slot(wave_base);
+            const uint32_t hid = lds_hid[sl];
+            if (ballot(seg && hid != ~0u)) key0 = hint_candidate<FAST>(seg && hid != ~0u, lds_pn[sl], hid, o, d, rd);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, tw, key0);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
-            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr, no_hit());
         }
         stamp(2);
         {
@@ -1122,6 +1188,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     att = att * mk(md.x, md.y, md.z);           // main.cxx:65 (unused if absorbed)
                     // raytracer.hxx:120-199
                     o = hp;
+                    if (kind != 2u) lds_hid[thread_slot(wave_base)] = ~0u;  // no hint after lambert, metal
                     if (kind == 0u) {                           // lambert, :132-141
                         RT_EV(EV_LAMBERT);
                         d = hp + hn;                            // + rius next iteration, then - p
@@ -1146,6 +1213,11 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
                             RT_EV(EV_DIELECTRIC);
+                            {   // the next segment tests this sphere first (hint_candidate)
+                                const uint32_t sl = thread_slot(wave_base);
+                                lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);  // its geo entry, raytracer.hxx:58
+                                lds_hid[sl] = ib;
+                            }
                             // {1 / ior, x(ior), x(1 / ior)} of this sphere, x(r) = (1 - r) / (1 + r)
                             const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
                             float4 dcs;
@@ -1573,7 +1645,8 @@ __global__ __launch_bounds__(256, 6) void wave_bounce_kernel(const KWave w)
         const float a = d.x * d.x + d.y * d.y + d.z * d.z;
         const uint64_t segm = ballot(seg);
         const RayDiv rd = ray_div(a, segm, p.fast_roots);
-        Hit h = closest_hit<false, CULL, false, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, CULL ? tw : nullptr);
+        Hit h = closest_hit<false, CULL, false, COUNT>(p, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, CULL ? tw : nullptr,
+                                                        no_hit());
         if (!seg) h = Hit{kNoHit};
         {
             const uint32_t ns = lanes(seg);

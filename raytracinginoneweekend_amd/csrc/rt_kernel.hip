@@ -1617,8 +1617,6 @@ __global__ __launch_bounds__(256, 6) void wave_bounce_kernel(const KWave w)
     for (uint32_t i = threadIdx.x; i < p.lds_units; i += blockDim.x) lds_blob[i] = p.blob[i];
     __syncthreads();
     const float4 *blob = lds_blob;
-    typedef const __attribute__((address_space(4))) KParams *kp_ptr_t;
-    const kp_ptr_t kp_base = (kp_ptr_t)__builtin_amdgcn_kernarg_segment_ptr();
     const float4 *geo = blob;
     const uint32_t *sidx = reinterpret_cast<const uint32_t *>(blob + p.n_geo);
     const float4 *clus = blob + p.clus_offset;

@@ -14,7 +14,7 @@ for r in $(seq 1 "${ROUNDS:-3}"); do
     if [ "$lib" = default ]; then unset RT_LIB_PATH; else export RT_LIB_PATH=$PWD/$lib; fi
     timeout -k 10 200 python bench.py --no-cpu-baseline --corrected-steps 0 --digest ${ARGS:-} > "$f" 2>&1
     rc=$?; if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $lib"; tail -5 "$f"; exit $rc; fi
-    grep '^{' "$f" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print('r$r', '$lib', r['ms_per_step'], r['frame_device_ms'], r['value'], r['parity']['frame_sha256'][:16], r['parity'].get('matches_reference'), r['segments_per_primary'])"
+    grep '^{' "$f" | python -c "import json,sys; r=json.loads(sys.stdin.read()); print('r$r', '$lib', r['ms_per_step'], r['frame_device_ms'], r['value'], r['parity'].get('frame_sha256','')[:16], r['parity'].get('matches_reference'), r['segments_per_primary'])"
   done
 done
 unset RT_LIB_PATH

@@ -87,6 +87,7 @@ struct KParams {
     uint32_t n_geo, n_always, n_clusters, clus_offset;
     uint32_t n_supers, supers_offset;  // level 2: groups of 4 consecutive clusters, 2 float4 each
     uint32_t use_root;       // level 3: one box over all clusters at supers_offset + 2 n_supers
+    uint32_t iso;            // isolated-sphere shortcut of the walk (rt_kernel.hip hint_candidate)
     uint32_t transpose_max;  // clusters requested by at most this many lanes (<= 16) are tested transposed
     uint32_t fast_roots;     // scene and camera within 2^19 of the origin: short exact root forms (rt_kernel.hip RayDiv)
     float clus_pad;          // max over clusters of 1e-3 * (|C|_1 + |e|_1) + 1e-6 (per-ray pad adds 1e-3 |o|_1)
@@ -168,6 +169,10 @@ struct KWave {
     uint32_t cap;            // queue capacity (rays)
     uint32_t item_begin, n_chunk;  // wave_gen_kernel: items [item_begin, item_begin + n_chunk)
 };
+
+// A lane inside an isolated dielectric sphere (rt_host.cpp isolated_spheres) skips the cluster
+// walk when both ends of its segment lie within the ball |p - C|^2 <= fl(fl(r r) kIsoR2Grow)
+constexpr float kIsoR2Grow = 1.0201f;
 
 // queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise
 constexpr uint32_t kQueueStride = 64;

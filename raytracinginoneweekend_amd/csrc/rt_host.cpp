@@ -388,6 +388,7 @@ struct blob_t {
     uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0, n_clusters_real = 0;
     uint32_t n_supers = 0, supers_offset = 0, shade_offset = 0;
     float clus_pad = 0.f;
+    std::vector<uint32_t> always;  // sphere indices tested on every segment (not clustered)
 };
 
 constexpr float kPadRel = 1e-3f;      // must match RT_PAD_REL in rt_kernel.hip
@@ -475,6 +476,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     };
     blob_t b;
     push(always);
+    b.always = always;
     b.n_always = static_cast<uint32_t>(always.size());  // tested with its exact count (padding after it)
     std::vector<float> crec;
     std::vector<float> boxes;  // per cluster lo/hi (6 floats), for the level-2 boxes
@@ -582,6 +584,59 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
         b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
     }
     return b;
+}
+
+// Isolated dielectric spheres (rt_kernel.hip hint_candidate): a lane whose last hit was such a
+// sphere S, whose next segment (0, 1.002 t] up to S's candidate t lies in the ball B(C, R_k)
+// (R_k^2 = fl(fl(r r) kIsoR2Grow), the kernel's check of both ends), skips the cluster walk. That
+// is exact when every clustered sphere T != S has its AABB, grown by the walk's own box pad for
+// any origin in the ball, disjoint from the ball: the segment then misses every padded box the
+// walk would test for T, and the walk's culling argument (such a T's candidate
+// cannot beat t) holds sphere by sphere. R adds to R_k a margin for the float rounding of the
+// kernel's check (a few ulp of |C| + r). Spheres tested on every segment (the ground) are
+// tested anyway. O(dielectric x clustered spheres) once per scene.
+std::vector<uint8_t> isolated_spheres(const rt_sphere *s, uint32_t n, const rt_material *m, const blob_t &b)
+{
+    std::vector<uint8_t> iso(n, 0);
+    if (b.n_clusters_real == 0) return iso;  // no walk to skip
+    std::vector<uint8_t> in_always(n, 0);
+    for (uint32_t i : b.always) in_always[i] = 1;
+    std::vector<uint32_t> others;
+    size_t n_diel = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!in_always[i]) others.push_back(i);
+        if (m[s[i].material].kind == RT_DIELECTRIC) ++n_diel;
+    }
+    if (static_cast<double>(n_diel) * static_cast<double>(others.size()) > 4e8) return iso;  // leave huge scenes alone
+    for (uint32_t S = 0; S < n && S < 0x7fffffffu; ++S) {
+        if (m[s[S].material].kind != RT_DIELECTRIC) continue;
+        const float r2 = s[S].radius * s[S].radius;  // the hint's geo entry, raytracer.hxx:58
+        const float r2k = r2 * rt::kIsoR2Grow;        // the kernel's check radius, squared
+        const double cx = s[S].center[0], cy = s[S].center[1], cz = s[S].center[2];
+        if (!std::isfinite(cx) || !std::isfinite(cy) || !std::isfinite(cz) || !std::isfinite(r2k)) continue;
+        const double rk = std::sqrt(static_cast<double>(r2k));
+        const double c1 = std::fabs(cx) + std::fabs(cy) + std::fabs(cz);
+        const double R = rk * (1.0 + 1e-5) + 1e-5 * (c1 + 2.0 * rk) + 1e-30;
+        const double pad = 1e-3 * (c1 + 2.0 * R) + static_cast<double>(b.clus_pad) + 1e-6;
+        const double C[3] = {cx, cy, cz};
+        bool ok = true;
+        for (uint32_t T : others) {
+            if (T == S) continue;
+            const double rt_ = std::fabs(static_cast<double>(s[T].radius));
+            double d2 = 0.0;
+            for (int a = 0; a < 3; ++a) {
+                const double lo = s[T].center[a] - rt_ - pad, hi = s[T].center[a] + rt_ + pad;
+                const double e = C[a] < lo ? lo - C[a] : (C[a] > hi ? C[a] - hi : 0.0);
+                d2 += e * e;
+            }
+            if (!(d2 > R * R * (1.0 + 1e-9))) {
+                ok = false;
+                break;
+            }
+        }
+        iso[S] = ok ? 1 : 0;
+    }
+    return iso;
 }
 
 uint32_t rows_of(const rt_params &p)
@@ -737,6 +792,14 @@ uint32_t deep_region_cap(uint32_t n_items)
 uint32_t deep_prio_env()
 {
     const char *e = std::getenv("RT_DEEP_PRIO");
+    return e && e[0] == '0' ? 0u : 1u;
+}
+
+// RT_ISO=0 turns off the isolated-sphere shortcut of the cluster walk (rt_kernel.hip
+// hint_candidate; A/B and tests; default on)
+uint32_t iso_env()
+{
+    const char *e = std::getenv("RT_ISO");
     return e && e[0] == '0' ? 0u : 1u;
 }
 
@@ -931,6 +994,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         std::memcpy(h + 8, &mt.kind, 4);
     }
     blob_t blobs[2] = {build_blob(spheres, n_spheres, false), build_blob(spheres, n_spheres, true)};
+    const std::vector<uint8_t> iso = isolated_spheres(spheres, n_spheres, materials, blobs[1]);
     // shading records join each blob (so they sit in LDS next to the geometry): per original
     // sphere index {c, r}, {albedo, param}, then the material kinds as bytes, 16-B padded
     for (blob_t &b : blobs) {
@@ -942,8 +1006,9 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         b.data.resize(at + kinds.size() / 4);
         std::memcpy(b.data.data() + at, kinds.data(), kinds.size());
         // dielectric constants per sphere index (raytracer.hxx:166-174 and the Schlick ratio
-        // :47): {1 / ior, (1 - ior) / (1 + ior), (1 - 1/ior) / (1 + 1/ior), 0}, the same
-        // binary32 operations the kernel would run (this file is built with -ffp-contract=off)
+        // :47): {1 / ior, (1 - ior) / (1 + ior), (1 - 1/ior) / (1 + 1/ior), isolated}, the same
+        // binary32 operations the kernel would run (this file is built with -ffp-contract=off);
+        // isolated = 1 for a sphere whose walk shortcut is exact (isolated_spheres)
         for (uint32_t i = 0; i < n_spheres; ++i) {
             const rt_material &mt = materials[spheres[i].material];
             float dc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -952,6 +1017,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
                 dc[0] = inv;
                 dc[1] = (1.f - ior) / (1.f + ior);
                 dc[2] = (1.f - inv) / (1.f + inv);
+                dc[3] = iso[i] ? 1.f : 0.f;
             }
             b.data.insert(b.data.end(), dc, dc + 4);
         }
@@ -1135,6 +1201,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     k.n_supers = sc->n_supers[b];
     k.supers_offset = sc->supers_offset[b];
     k.use_root = root_box_env();
+    k.iso = iso_env();
     k.transpose_max = transpose_max_env();
     k.fast_roots = sc->in_fast_range && camera_in_fast_range(*camera) && fast_roots_env() ? 1u : 0u;
     k.shade_offset = sc->shade_offset[b];

@@ -72,6 +72,8 @@ enum DbgEvent : uint32_t {
     EV_LIVE_LANES,  // live lanes summed over wave iterations
     EV_DRY_ITER,    // wave iterations after the item queues ran dry (the drain)
     EV_DRY_LANES,   // live lanes summed over those
+    EV_ISO_LANES,   // lanes that skipped the cluster walk (isolated hint sphere), summed over iterations
+    EV_WALK_SKIPPED,  // wave iterations with segments whose cluster walk no lane needed
     EV_COUNT
 };
 static_assert(EV_COUNT <= kDbgEvents, "event counters");
@@ -612,10 +614,20 @@ __device__ __forceinline__ void cluster_members7(bool req, uint64_t M, uint32_t 
 // The candidate is the reference's (raytracer.hxx:55-90, the op sequence of test_block8 on
 // the sphere's geo entry {C, fl(r r)}), so the (t, index) minimum is unchanged when the walk
 // meets the sphere again. hint: this lane's last hit was a dielectric sphere, whose geo entry
-// and original index wait in the lane's LDS slots.
+// and original index (hid; bit 31: the sphere is isolated) wait in the lane's LDS slots.
+//
+// Isolated spheres (rt_host.cpp isolated_spheres; KParams::iso): when the segment (0, 1.002 t]
+// up to the sphere's own candidate t lies in the ball |p - C|^2 <= fl(r r) kIsoR2Grow (both ends
+// checked; the ball is convex), the host has shown that it misses every other clustered sphere's
+// padded box, so the walk would cull every cluster but for this sphere, whose key is already
+// found: `skip` = the lane needs no walk (the always-tested spheres are still tested). A ray
+// trapped in a small glass ball (the reference's refract) takes this path for every bounce.
 template <bool FAST>
-__device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t id, f3 o, f3 d, const RayDiv &rd)
+__device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t hid, f3 o, f3 d, const RayDiv &rd,
+                                                   uint32_t iso, bool &skip)
 {
+    const uint32_t id = hid & 0x7fffffffu;
+    skip = false;
     const float a = rd.a;
     const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;            // raytracer.hxx:55
     float b, disc;
@@ -643,7 +655,17 @@ __device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t
     }
     const uint64_t kt = hit_key(t, id);
     const uint64_t none = no_hit();
-    return kt < none ? kt : none;  // a NaN key (no candidate) orders above kNoHit: none then
+    const uint64_t key = kt < none ? kt : none;  // a NaN key (no candidate) orders above kNoHit: none then
+    if (iso && ballot(pos && (int32_t)hid < 0)) {
+        // a valid key implies pos, hence hint; t then is finite and in range
+        const float tq = t * 1.002f;  // the walk's bound, h.t() * 1.002f
+        const float qx = fmaf(tq, d.x, ocx), qy = fmaf(tq, d.y, ocy), qz = fmaf(tq, d.z, ocz);
+        const float r2k = s.w * kIsoR2Grow;
+        const float o2 = ocx * ocx + ocy * ocy + ocz * ocz;
+        const float q2 = qx * qx + qy * qy + qz * qz;
+        skip = (int32_t)hid < 0 && key < none && o2 <= r2k && q2 <= r2k;
+    }
+    return key;
 }
 
 template <bool FAST, int CULL, bool STATS, bool COUNT, class KP>
@@ -674,7 +696,9 @@ __device__ __forceinline__ Hit closest_hit(const KP &p, const float4 *__restrict
         const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
         const float4 *sup = clus + (p.supers_offset - p.clus_offset);
         uint32_t n_supers = p.n_supers;
-        if (p.use_root) {
+        if (!am) {
+            n_supers = 0;  // every lane's segment is settled (isolated hint spheres)
+        } else if (p.use_root) {
             wt.add_box(lanes(active));
             if (!(ballot(box_pass(rb, sup[2 * p.n_supers], sup[2 * p.n_supers + 1], t_lo, h.t() * 1.002f)) & am))
                 n_supers = 0;
@@ -925,7 +949,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     // its hint sphere (hint_candidate): the geo entry from the shading record
                     const uint32_t hid = P.deep.hid[I], sl = thread_slot(wave_base);
                     if (hid != ~0u) {
-                        const float4 sf = gld4(P.blob + P.shade_offset, 2u * hid);
+                        const float4 sf = gld4(P.blob + P.shade_offset, 2u * (hid & 0x7fffffffu));
                         lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);
                     }
                     lds_hid[sl] = hid;
@@ -1111,10 +1135,18 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         Hit h{kNoHit};
         if constexpr (CULL == 7) {  // whole wave: every lane helps with transposed member tests
             uint64_t key0 = no_hit();
+            bool skip = false;
             const uint32_t sl = thread_slot(wave_base);
             const uint32_t hid = lds_hid[sl];
-            if (ballot(seg && hid != ~0u)) key0 = hint_candidate<FAST>(seg && hid != ~0u, lds_pn[sl], hid, o, d, rd);
-            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, seg, segm, tw, key0);
+            if (ballot(seg && hid != ~0u))
+                key0 = hint_candidate<FAST>(seg && hid != ~0u, lds_pn[sl], hid, o, d, rd, P.iso, skip);
+            const bool walk = seg && !skip;
+            const uint64_t wm = ballot(walk);
+            if (STATS && first_active_lane()) {
+                dbg.ev[EV_ISO_LANES] += (uint32_t)__popcll(segm & ~wm);
+                if (segm && !wm) ++dbg.ev[EV_WALK_SKIPPED];
+            }
+            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
             h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr, no_hit());
@@ -1213,12 +1245,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
                             RT_EV(EV_DIELECTRIC);
-                            {   // the next segment tests this sphere first (hint_candidate)
-                                const uint32_t sl = thread_slot(wave_base);
-                                lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);  // its geo entry, raytracer.hxx:58
-                                lds_hid[sl] = ib;
-                            }
-                            // {1 / ior, x(ior), x(1 / ior)} of this sphere, x(r) = (1 - r) / (1 + r)
+                            // {1 / ior, x(ior), x(1 / ior), isolated} of this sphere, x(r) = (1 - r) / (1 + r)
                             const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
                             float4 dcs;
                             if (V != V_EXACT_SCALAR && P.shade_lds) {
@@ -1226,6 +1253,11 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                                 asm volatile("");  // no merged (flat) load, as above
                             } else {
                                 dcs = gld4(P.blob, di);
+                            }
+                            {   // the next segment tests this sphere first (hint_candidate)
+                                const uint32_t sl = thread_slot(wave_base);
+                                lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);  // its geo entry, raytracer.hxx:58
+                                lds_hid[sl] = ib | (dcs.w != 0.f ? 0x80000000u : 0u);
                             }
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w, xs = dcs.y;

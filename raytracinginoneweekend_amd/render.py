@@ -184,7 +184,8 @@ class DeviceScene:
 
     EVENTS = ["iter", "refill_trip", "fresh", "reject_trip", "lens_done", "scatter_done", "root_gate_pass", "super",
               "super_pass", "cluster_req", "transposed", "t_round", "t_far", "per_lane_members", "sky", "hit",
-              "lambert", "unit_dir", "dielectric", "store", "metal_absorb", "live_lanes", "dry_iter", "dry_lanes"]
+              "lambert", "unit_dir", "dielectric", "store", "metal_absorb", "live_lanes", "dry_iter", "dry_lanes",
+              "iso_lanes", "walk_skipped"]
 
     def debug_events(self, reset=True):
         """Block-execution counts of the instrumented kernel (RT_DEBUG_STATS=1), see rt_scene_debug_events."""

@@ -227,6 +227,83 @@ def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, transpose, 
     assert st.segments == seg
 
 
+def _glass_scene(rng, n, spread):
+    """Small glass balls, the domain of the isolated-sphere shortcut (hint_candidate): isolated
+    balls resting on the ground (as in the reference's huge scene), touching and overlapping
+    neighbours, a ball with a bubble (negative radius) inside, exact duplicates, a big glass
+    sphere, a few lambert/metal balls and the ground."""
+    s = np.zeros(n, dtype=abi.SPHERE_DTYPE)
+    m = np.zeros(5, dtype=abi.MATERIAL_DTYPE)
+    m[0] = (0, [0.5, 0.5, 0.5], 0.0)
+    m[1] = (1, [0.7, 0.6, 0.5], 0.1)
+    m[2] = (2, [1.0, 1.0, 1.0], 1.5)
+    m[3] = (2, [1.0, 1.0, 1.0], 1.33)
+    m[4] = (0, [0.8, 0.3, 0.2], 0.0)
+    r = rng.choice([0.2, 0.2, 0.2, 0.1, 0.35], n).astype(np.float32)
+    c = np.zeros((n, 3), dtype=np.float32)
+    c[:, 0] = rng.uniform(-spread, spread, n)
+    c[:, 2] = rng.uniform(-spread, spread, n)
+    c[:, 1] = r
+    mat = rng.choice([2, 2, 3, 3, 2, 0, 1, 4], n)
+    k = n // 8
+    c[2:2 + k:2, 0] = c[3:3 + k:2, 0] + (r[2:2 + k:2] + r[3:3 + k:2])  # touching pairs (in float)
+    c[2:2 + k:2, 2] = c[3:3 + k:2, 2]
+    c[2 + k:2 + 2 * k:2, 0] = c[3 + k:3 + 2 * k:2, 0] + 0.5 * (r[2 + k:2 + 2 * k:2] + r[3 + k:3 + 2 * k:2])  # overlapping
+    c[2 + k:2 + 2 * k:2, 2] = c[3 + k:3 + 2 * k:2, 2]
+    c[5 * k], r[5 * k], mat[5 * k] = c[5 * k + 1], -0.8 * r[5 * k + 1], 2  # bubble in ball 5k + 1
+    mat[5 * k + 1] = 2
+    c[6 * k], r[6 * k] = c[6 * k + 1], r[6 * k + 1]                   # exact duplicate
+    s["center"], s["radius"], s["material"] = c, r, mat
+    s["center"][0], s["radius"][0], s["material"][0] = (0, -1000, 0), 1000.0, 0
+    s["center"][1], s["radius"][1], s["material"][1] = (0, 1, 0), 1.0, 2
+    return s, m
+
+
+@pytest.mark.parametrize("seed,n,spread,mode,taken", [(7, 300, 12.0, abi.RT_CAMERA_REFERENCE, True),
+                                                      (8, 500, 14.0, abi.RT_CAMERA_CORRECTED, True),
+                                                      (9, 200, 8.0, abi.RT_CAMERA_CORRECTED, True),
+                                                      (7, 400, 6.0, abi.RT_CAMERA_REFERENCE, False)])  # dense
+def test_isolated_sphere_shortcut_is_bit_exact(seed, n, spread, mode, taken, monkeypatch):
+    """Paths trapped in small glass balls skip the cluster walk when their segment stays inside
+    an isolated ball (RT_ISO, default on): the same bits as without the shortcut, as brute force
+    and as the oracle, with the deep-path split at 3 segments (the deep launch takes the
+    shortcut too); the instrumented kernel shows lanes taking it."""
+    rng = np.random.default_rng(seed)
+    s, m = _glass_scene(rng, n, spread)
+    W, H, spp = 48, 32, 8
+    cam = O.camera_default(W, H, mode)
+    p = rt.make_params(W, H, spp, 64, seed)
+    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
+    monkeypatch.setenv("RT_DEEP_SPLIT", "3")
+    on, st = rt.render_f32((s, m), p, cam)
+    monkeypatch.setenv("RT_ISO", "0")
+    off, so = rt.render_f32((s, m), p, cam)
+    monkeypatch.delenv("RT_ISO")
+    _bits_equal(on, off)
+    assert st.segments == so.segments
+    assert st.box_tests <= so.box_tests
+    if taken:
+        assert st.box_tests < so.box_tests  # the shortcut was taken
+    brute, sb = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, seed, brute_force=True), cam)
+    _bits_equal(on, brute)
+    ref, seg = O.render_f32(s, m, cam, p)
+    _bits_equal(on, ref)
+    assert st.segments == seg == sb.segments
+    # the instrumented kernel: lanes took the shortcut, and whole iterations skipped the walk
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("RT_DEBUG_STATS", "1")
+    ds = rt.DeviceScene((s, m))
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    ds.render(rt.Camera.default(W, H, mode), p, out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ev = ds.debug_events(reset=True)
+    ds.close()
+    _bits_equal(out.cpu().numpy(), ref)
+    if taken:
+        assert ev["iso_lanes"] > 0 and ev["walk_skipped"] > 0, ev
+
+
 # ---- fast-math kernel: stated tolerance (SURVEY.md §8c "performance build") ---------------
 # FMA-contracted discriminant, v_sqrt_f32 and reciprocal roots move hit times by a few ulp;
 # a path whose hit/miss or reflect/refract decision flips diverges, so the bound is on the

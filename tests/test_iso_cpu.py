@@ -1,0 +1,115 @@
+"""The isolated-sphere shortcut (rt_kernel.hip hint_candidate, rt_host.cpp isolated_spheres),
+checked as a geometric claim on the CPU with the reference's own binary32 arithmetic.
+
+A lane whose last hit was a dielectric sphere S tests S first; when S is isolated (every other
+clustered sphere's AABB, grown by the walk's box pad for any origin in the ball, is disjoint from
+the ball |p - C|^2 <= fl(fl(r r) 1.0201) plus a rounding margin) and both ends of the lane's
+segment (0, fl(1.002 t_S)] lie in that ball, the kernel skips the cluster walk. The claim: then no
+other clustered sphere's candidate (raytracer.hxx:52-91: near root in (kMIN, kMAX), else far
+root) beats S's in the (t, index) order of closest_hit (raytracer.hxx:94-118). Here rays start
+on (and a few ulp off) the isolated spheres of the reference's huge scene, in every direction
+including near-tangent ones, with |d| from 0.3 to 6; S's candidate and every other sphere's are
+computed op by op in binary32, and every ray that passes the kernel's check is verified.
+(The GPU tests check the kernel's bits with and without the shortcut.)"""
+import numpy as np
+
+import golden_io as G
+
+KMIN = np.float32(0.008)
+GROW = np.float32(1.0201)  # rt_device.h kIsoR2Grow
+
+
+def _cand(o, d, C, r):
+    """The reference's candidate t of each (ray, sphere), inf when none; binary32 op by op."""
+    f = np.float32
+    ocx, ocy, ocz = (o[:, None, k] - C[None, :, k] for k in range(3))
+    dx, dy, dz = (d[:, None, k] for k in range(3))
+    a = (dx * dx + dy * dy) + dz * dz
+    b = (ocx * dx + ocy * dy) + ocz * dz
+    c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - (r * r)[None, :]
+    disc = b * b - a * c
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        q = np.sqrt(np.where(disc > 0, disc, f(0)))
+        t1 = (-b - q) / a
+        t2 = (-b + q) / a
+    fmax = np.float32(np.finfo(np.float32).max)
+    ok1 = (disc > 0) & (t1 > KMIN) & (t1 < fmax)
+    ok2 = (disc > 0) & ~ok1 & (t2 > KMIN) & (t2 < fmax)
+    return np.where(ok1, t1, np.where(ok2, t2, np.float32(np.inf))).astype(np.float32)
+
+
+def _fma32(a, b, c):
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
+
+
+def _isolated(C, r, always, kinds, pad0):
+    """rt_host.cpp isolated_spheres, in double."""
+    iso = np.zeros(len(r), dtype=bool)
+    others = np.where(~always)[0]
+    ra = np.abs(r.astype(np.float64))
+    for S in np.where(kinds == 2)[0]:
+        r2k = np.float32(np.float32(r[S] * r[S]) * GROW)
+        rk = np.sqrt(np.float64(r2k))
+        c1 = np.abs(C[S].astype(np.float64)).sum()
+        R = rk * (1 + 1e-5) + 1e-5 * (c1 + 2 * rk) + 1e-30
+        pad = 1e-3 * (c1 + 2 * R) + pad0 + 1e-6
+        T = others[others != S]
+        lo = C[T].astype(np.float64) - ra[T, None] - pad
+        hi = C[T].astype(np.float64) + ra[T, None] + pad
+        x = C[S].astype(np.float64)
+        e = np.maximum(np.maximum(lo - x, 0.0), x - hi)
+        iso[S] = bool(((e * e).sum(1) > R * R * (1 + 1e-9)).all())
+    return iso
+
+
+def test_isolated_sphere_claim_huge_scene():
+    s, m = G.scene("huge")
+    C = np.ascontiguousarray(s["center"], dtype=np.float32)
+    r = np.ascontiguousarray(s["radius"], dtype=np.float32)
+    kinds = m["kind"][s["material"]]
+    ra = np.abs(r)
+    always = ra > 64 * np.median(ra)  # rt_host.cpp build_blob: the ground
+    # the walk's box pad: at least the level-3 box's (the max over the scene's boxes)
+    lo = (C - ra[:, None])[~always].min(0)
+    hi = (C + ra[:, None])[~always].max(0)
+    cc, ee = 0.5 * (lo + hi), 0.5 * (hi - lo)
+    pad0 = 1e-3 * (np.abs(cc).sum() + ee.sum()) + 1e-6
+    iso = _isolated(C, r, always, kinds, pad0)
+    assert iso.sum() >= 80  # most of the scene's glass balls
+    others = np.where(~always)[0]
+    rng = np.random.default_rng(2024)
+    checked = 0
+    for S in np.where(iso)[0]:
+        n = 1500
+        u = rng.normal(size=(n, 3))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        o = (C[S][None, :].astype(np.float64) + ra[S] * u).astype(np.float32)
+        o = (o.view(np.int32) + rng.integers(-3, 4, size=o.shape).astype(np.int32)).view(np.float32)  # a few ulp off
+        v = rng.normal(size=(n, 3))
+        v /= np.linalg.norm(v, axis=1, keepdims=True)
+        # a third near-tangent: the direction nearly in the tangent plane at o
+        tang = v - (v * u).sum(1, keepdims=True) * u
+        tang /= np.linalg.norm(tang, axis=1, keepdims=True)
+        k = n // 3
+        v[:k] = tang[:k] + rng.uniform(-1e-3, 1e-3, (k, 1)) * u[:k]
+        d = (v * rng.uniform(0.3, 6.0, (n, 1))).astype(np.float32)
+        tS = _cand(o, d, C[S:S + 1], r[S:S + 1])[:, 0]
+        valid = np.isfinite(tS)
+        # the kernel's check (hint_candidate): both ends of (0, fl(1.002 t)] in the ball
+        oc = o - C[S][None, :]
+        tq = (tS * np.float32(1.002)).astype(np.float32)
+        q = _fma32(np.where(valid, tq, 0)[:, None], d, oc)
+        o2 = (oc[:, 0] * oc[:, 0] + oc[:, 1] * oc[:, 1]) + oc[:, 2] * oc[:, 2]
+        q2 = (q[:, 0] * q[:, 0] + q[:, 1] * q[:, 1]) + q[:, 2] * q[:, 2]
+        r2k = np.float32(np.float32(r[S] * r[S]) * GROW)
+        skip = valid & (o2 <= r2k) & (q2 <= r2k)
+        if not skip.any():
+            continue
+        T = others[others != S]
+        tT = _cand(o[skip], d[skip], C[T], r[T])
+        # (t, index) order: T beats S if t_T < t_S, or t_T == t_S and T < S
+        beats = (tT < tS[skip, None]) | ((tT == tS[skip, None]) & (T[None, :] < S))
+        assert not beats.any(), f"sphere {S}: {int(beats.sum())} candidates beat the isolated sphere"
+        checked += int(skip.sum())
+    assert checked > 50000, checked
+    print(f"isolated glass spheres {int(iso.sum())}, rays checked {checked}")

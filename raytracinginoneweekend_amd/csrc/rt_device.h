@@ -173,6 +173,9 @@ struct KWave {
 // A lane inside an isolated dielectric sphere (rt_host.cpp isolated_spheres) skips the cluster
 // walk when both ends of its segment lie within the ball |p - C|^2 <= fl(fl(r r) kIsoR2Grow)
 constexpr float kIsoR2Grow = 1.0201f;
+// a dielectric sphere's shortcut word (rt_host.cpp shortcut_words): this bit, then the geo slots
+// (+ 1, 0 = none) of its at most two neighbours in bits [0, 15) and [15, 30)
+constexpr uint32_t kShortcut = 0x80000000u;
 
 // queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise
 constexpr uint32_t kQueueStride = 64;

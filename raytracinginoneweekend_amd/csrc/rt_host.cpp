@@ -586,19 +586,32 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
     return b;
 }
 
-// Isolated dielectric spheres (rt_kernel.hip hint_candidate): a lane whose last hit was such a
-// sphere S, whose next segment (0, 1.002 t] up to S's candidate t lies in the ball B(C, R_k)
-// (R_k^2 = fl(fl(r r) kIsoR2Grow), the kernel's check of both ends), skips the cluster walk. That
-// is exact when every clustered sphere T != S has its AABB, grown by the walk's own box pad for
-// any origin in the ball, disjoint from the ball: the segment then misses every padded box the
-// walk would test for T, and the walk's culling argument (such a T's candidate
-// cannot beat t) holds sphere by sphere. R adds to R_k a margin for the float rounding of the
-// kernel's check (a few ulp of |C| + r). Spheres tested on every segment (the ground) are
-// tested anyway. O(dielectric x clustered spheres) once per scene.
-std::vector<uint8_t> isolated_spheres(const rt_sphere *s, uint32_t n, const rt_material *m, const blob_t &b)
+// The walk shortcut of dielectric spheres (rt_kernel.hip hint_candidate): a lane whose last hit
+// was such a sphere S, whose next segment (0, 1.002 t] up to S's candidate t lies in the ball
+// B(C, R_k) (R_k^2 = fl(fl(r r) kIsoR2Grow), the kernel's check of both ends), tests S's
+// neighbours instead of walking the clusters. The neighbours N(S) are the clustered spheres
+// T != S whose AABB, grown by the walk's own box pad for any origin in the ball, meets the ball;
+// for every other T the segment misses every padded box the walk would test, and the walk's
+// culling argument (such a T's candidate cannot beat t) holds sphere by sphere.
+// So the minimum over S, N(S) and the always-tested spheres (the ground, tested anyway) is the
+// walk's. R adds to R_k a margin for the float rounding of the kernel's check (a few ulp of
+// |C| + r). Per sphere: kShortcut | (geo slot of neighbour 0, + 1) | (slot of neighbour 1, + 1)
+// << 15 for spheres with at most two neighbours ("isolated": none), 0 otherwise.
+// O(dielectric x clustered spheres) once per scene.
+std::vector<uint32_t> shortcut_words(const rt_sphere *s, uint32_t n, const rt_material *m, const blob_t &b)
 {
-    std::vector<uint8_t> iso(n, 0);
-    if (b.n_clusters_real == 0) return iso;  // no walk to skip
+    std::vector<uint32_t> word(n, 0);
+    if (b.n_clusters_real == 0) return word;  // no walk to skip
+    // geo slot of each clustered sphere (blob layout: geo [n_geo] then sidx [n_geo])
+    std::vector<uint32_t> slot(n, ~0u);
+    for (uint32_t g = 0; g < b.n_geo; ++g) {
+        uint32_t id;
+        std::memcpy(&id, &b.data[4u * b.n_geo + g], 4);
+        if (id < n && g >= b.n_always) slot[id] = g;
+    }
+    const bool slots_fit = b.n_geo < 0x7fffu;
+    const char *e = std::getenv("RT_ISO_NB");  // RT_ISO_NB=0: isolated spheres only (A/B)
+    const bool nb_off = e && e[0] == '0';
     std::vector<uint8_t> in_always(n, 0);
     for (uint32_t i : b.always) in_always[i] = 1;
     std::vector<uint32_t> others;
@@ -607,7 +620,7 @@ std::vector<uint8_t> isolated_spheres(const rt_sphere *s, uint32_t n, const rt_m
         if (!in_always[i]) others.push_back(i);
         if (m[s[i].material].kind == RT_DIELECTRIC) ++n_diel;
     }
-    if (static_cast<double>(n_diel) * static_cast<double>(others.size()) > 4e8) return iso;  // leave huge scenes alone
+    if (static_cast<double>(n_diel) * static_cast<double>(others.size()) > 4e8) return word;  // leave huge scenes alone
     for (uint32_t S = 0; S < n && S < 0x7fffffffu; ++S) {
         if (m[s[S].material].kind != RT_DIELECTRIC) continue;
         const float r2 = s[S].radius * s[S].radius;  // the hint's geo entry, raytracer.hxx:58
@@ -619,6 +632,7 @@ std::vector<uint8_t> isolated_spheres(const rt_sphere *s, uint32_t n, const rt_m
         const double R = rk * (1.0 + 1e-5) + 1e-5 * (c1 + 2.0 * rk) + 1e-30;
         const double pad = 1e-3 * (c1 + 2.0 * R) + static_cast<double>(b.clus_pad) + 1e-6;
         const double C[3] = {cx, cy, cz};
+        uint32_t nb[2], n_nb = 0;
         bool ok = true;
         for (uint32_t T : others) {
             if (T == S) continue;
@@ -630,13 +644,18 @@ std::vector<uint8_t> isolated_spheres(const rt_sphere *s, uint32_t n, const rt_m
                 d2 += e * e;
             }
             if (!(d2 > R * R * (1.0 + 1e-9))) {
-                ok = false;
-                break;
+                if (n_nb == 2 || !slots_fit || slot[T] == ~0u) {
+                    ok = false;
+                    break;
+                }
+                nb[n_nb++] = slot[T];
             }
         }
-        iso[S] = ok ? 1 : 0;
+        if (ok && n_nb && nb_off) ok = false;
+        if (ok)
+            word[S] = rt::kShortcut | (n_nb > 0 ? nb[0] + 1u : 0u) | (n_nb > 1 ? (nb[1] + 1u) << 15 : 0u);
     }
-    return iso;
+    return word;
 }
 
 uint32_t rows_of(const rt_params &p)
@@ -994,7 +1013,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         std::memcpy(h + 8, &mt.kind, 4);
     }
     blob_t blobs[2] = {build_blob(spheres, n_spheres, false), build_blob(spheres, n_spheres, true)};
-    const std::vector<uint8_t> iso = isolated_spheres(spheres, n_spheres, materials, blobs[1]);
+    const std::vector<uint32_t> shortcut = shortcut_words(spheres, n_spheres, materials, blobs[1]);
     // shading records join each blob (so they sit in LDS next to the geometry): per original
     // sphere index {c, r}, {albedo, param}, then the material kinds as bytes, 16-B padded
     for (blob_t &b : blobs) {
@@ -1006,9 +1025,9 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         b.data.resize(at + kinds.size() / 4);
         std::memcpy(b.data.data() + at, kinds.data(), kinds.size());
         // dielectric constants per sphere index (raytracer.hxx:166-174 and the Schlick ratio
-        // :47): {1 / ior, (1 - ior) / (1 + ior), (1 - 1/ior) / (1 + 1/ior), isolated}, the same
+        // :47): {1 / ior, (1 - ior) / (1 + ior), (1 - 1/ior) / (1 + 1/ior), shortcut}, the same
         // binary32 operations the kernel would run (this file is built with -ffp-contract=off);
-        // isolated = 1 for a sphere whose walk shortcut is exact (isolated_spheres)
+        // and the sphere's walk-shortcut word (shortcut_words; as raw bits)
         for (uint32_t i = 0; i < n_spheres; ++i) {
             const rt_material &mt = materials[spheres[i].material];
             float dc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1017,7 +1036,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
                 dc[0] = inv;
                 dc[1] = (1.f - ior) / (1.f + ior);
                 dc[2] = (1.f - inv) / (1.f + inv);
-                dc[3] = iso[i] ? 1.f : 0.f;
+                std::memcpy(&dc[3], &shortcut[i], 4);
             }
             b.data.insert(b.data.end(), dc, dc + 4);
         }

@@ -605,29 +605,12 @@ __device__ __forceinline__ void cluster_members7(bool req, uint64_t M, uint32_t 
     }
 }
 
-// The sphere a path last refracted into or reflected off inside (a dielectric hit), tested
-// first: a ray trapped in a small glass sphere (the reference's refract, raytracer.hxx:158-194,
-// keeps 0.17% of the samples bouncing up to max_depth, nearly all inside small dielectric
-// spheres) then starts the walk with t_best at that sphere's far wall, and the padded boxes of
-// every cluster its short segment does not reach are culled, where before the ground's or no
-// t_best let a wave's 64 paths request ~8 clusters per segment (deep launch, STATS events).
-// The candidate is the reference's (raytracer.hxx:55-90, the op sequence of test_block8 on
-// the sphere's geo entry {C, fl(r r)}), so the (t, index) minimum is unchanged when the walk
-// meets the sphere again. hint: this lane's last hit was a dielectric sphere, whose geo entry
-// and original index (hid; bit 31: the sphere is isolated) wait in the lane's LDS slots.
-//
-// Isolated spheres (rt_host.cpp isolated_spheres; KParams::iso): when the segment (0, 1.002 t]
-// up to the sphere's own candidate t lies in the ball |p - C|^2 <= fl(r r) kIsoR2Grow (both ends
-// checked; the ball is convex), the host has shown that it misses every other clustered sphere's
-// padded box, so the walk would cull every cluster but for this sphere, whose key is already
-// found: `skip` = the lane needs no walk (the always-tested spheres are still tested). A ray
-// trapped in a small glass ball (the reference's refract) takes this path for every bounce.
+// One sphere's candidate for this lane's segment (raytracer.hxx:55-90, the op sequence of
+// test_block8 on its geo entry {C, fl(r r)}) as a key, no_hit() without one. want: this lane
+// asks (the others compute along and get no_hit()); t: the candidate's t when the key is valid.
 template <bool FAST>
-__device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t hid, f3 o, f3 d, const RayDiv &rd,
-                                                   uint32_t iso, bool &skip)
+__device__ __forceinline__ uint64_t sphere_key(bool want, float4 s, uint32_t id, f3 o, f3 d, const RayDiv &rd, float &t)
 {
-    const uint32_t id = hid & 0x7fffffffu;
-    skip = false;
     const float a = rd.a;
     const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;            // raytracer.hxx:55
     float b, disc;
@@ -640,12 +623,13 @@ __device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t
         const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;             // :58
         disc = b * b - a * c;                                                // :60
     }
-    const bool pos = hint && disc > 0.f;                                     // :62
+    const bool pos = want && disc > 0.f;                                     // :62
     const uint64_t posm = ballot(pos);
+    t = 0.f;
     if (!posm) return no_hit();
     const float dk = pos ? disc : -1.f;  // NaN candidate without a positive discriminant
     float q;
-    float t = near_root(b, dk, rd, q);                                       // :63
+    t = near_root(b, dk, rd, q);                                             // :63
     const bool ok = in_range(t);
     if (posm & ~ballot(ok)) {
         const float t2 = far_root(b, q, rd);                                 // :76
@@ -655,15 +639,53 @@ __device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t
     }
     const uint64_t kt = hit_key(t, id);
     const uint64_t none = no_hit();
-    const uint64_t key = kt < none ? kt : none;  // a NaN key (no candidate) orders above kNoHit: none then
-    if (iso && ballot(pos && (int32_t)hid < 0)) {
-        // a valid key implies pos, hence hint; t then is finite and in range
+    return kt < none ? kt : none;  // a NaN key (no candidate) orders above kNoHit: none then
+}
+
+// The sphere a path last refracted into or reflected off inside (a dielectric hit), tested
+// first: a ray trapped in a small glass sphere (the reference's refract, raytracer.hxx:158-194,
+// keeps 0.17% of the samples bouncing up to max_depth, nearly all inside small dielectric
+// spheres) then starts the walk with t_best at that sphere's far wall, and the padded boxes of
+// every cluster its short segment does not reach are culled. The candidate is the reference's,
+// so the (t, index) minimum is unchanged when the walk meets the sphere again. hint: this lane's
+// last hit was a dielectric sphere, whose geo entry, original index (hid; kShortcut: the sphere
+// has a shortcut word) and shortcut word (nbw) wait in the lane's LDS slots.
+//
+// The shortcut (rt_host.cpp shortcut_words; KParams::iso): when the segment (0, 1.002 t] up to
+// the sphere's own candidate t lies in the ball |p - C|^2 <= fl(r r) kIsoR2Grow (both ends
+// checked; the ball is convex), the host has shown that it misses the padded box of every
+// clustered sphere but the sphere's at most two neighbours (none: "isolated"), whose slots nbw
+// holds: the lane tests them here and needs no walk (`skip`; the always-tested spheres are still
+// tested). A ray trapped in a small glass ball takes this path for every bounce.
+template <bool FAST>
+__device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t hid, uint32_t nbw,
+                                                   const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
+                                                   f3 o, f3 d, const RayDiv &rd, uint32_t iso, bool &skip)
+{
+    skip = false;
+    float t;
+    uint64_t key = sphere_key<FAST>(hint, s, hid & 0x7fffffffu, o, d, rd, t);
+    if (iso && ballot(key < no_hit() && (int32_t)hid < 0)) {
+        // a valid key implies hint; t then is finite and in range
+        const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
         const float tq = t * 1.002f;  // the walk's bound, h.t() * 1.002f
         const float qx = fmaf(tq, d.x, ocx), qy = fmaf(tq, d.y, ocy), qz = fmaf(tq, d.z, ocz);
         const float r2k = s.w * kIsoR2Grow;
         const float o2 = ocx * ocx + ocy * ocy + ocz * ocz;
         const float q2 = qx * qx + qy * qy + qz * qz;
-        skip = (int32_t)hid < 0 && key < none && o2 <= r2k && q2 <= r2k;
+        skip = (int32_t)hid < 0 && key < no_hit() && o2 <= r2k && q2 <= r2k;
+        // the neighbours (geo slots + 1 in nbw), tested by the lanes that skip the walk
+        const uint32_t n0 = nbw & 0x7fffu, n1 = (nbw >> 15) & 0x7fffu;
+        if (ballot(skip && n0 != 0u)) {
+            const uint32_t g = n0 ? n0 - 1u : 0u;
+            const uint64_t k = sphere_key<FAST>(skip && n0 != 0u, geo[g], sidx[g], o, d, rd, t);
+            if (k < key) key = k;
+        }
+        if (ballot(skip && n1 != 0u)) {
+            const uint32_t g = n1 ? n1 - 1u : 0u;
+            const uint64_t k = sphere_key<FAST>(skip && n1 != 0u, geo[g], sidx[g], o, d, rd, t);
+            if (k < key) key = k;
+        }
     }
     return key;
 }
@@ -788,6 +810,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     // the dielectric sphere the lane's path last hit (hint_candidate; its original index in lds_hid)
     __shared__ float4 lds_pn[256];
     __shared__ uint32_t lds_hid[256];
+    __shared__ uint32_t lds_nb[256];  // the dielectric sphere's shortcut word (hint_candidate)
     const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
     // the deep launch's waves issue ahead of other launches' waves (KParams::deep_prio): each of
@@ -949,8 +972,11 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     // its hint sphere (hint_candidate): the geo entry from the shading record
                     const uint32_t hid = P.deep.hid[I], sl = thread_slot(wave_base);
                     if (hid != ~0u) {
-                        const float4 sf = gld4(P.blob + P.shade_offset, 2u * (hid & 0x7fffffffu));
+                        const uint32_t ib = hid & 0x7fffffffu;
+                        const float4 sf = gld4(P.blob + P.shade_offset, 2u * ib);
                         lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);
+                        const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
+                        lds_nb[sl] = __float_as_uint(gld4(P.blob, di).w);
                     }
                     lds_hid[sl] = hid;
                 } else {
@@ -1139,7 +1165,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             const uint32_t sl = thread_slot(wave_base);
             const uint32_t hid = lds_hid[sl];
             if (ballot(seg && hid != ~0u))
-                key0 = hint_candidate<FAST>(seg && hid != ~0u, lds_pn[sl], hid, o, d, rd, P.iso, skip);
+                key0 = hint_candidate<FAST>(seg && hid != ~0u, lds_pn[sl], hid, lds_nb[sl], geo, sidx, o, d, rd, P.iso, skip);
             const bool walk = seg && !skip;
             const uint64_t wm = ballot(walk);
             if (STATS && first_active_lane()) {
@@ -1245,7 +1271,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
                             RT_EV(EV_DIELECTRIC);
-                            // {1 / ior, x(ior), x(1 / ior), isolated} of this sphere, x(r) = (1 - r) / (1 + r)
+                            // {1 / ior, x(ior), x(1 / ior), shortcut word} of this sphere, x(r) = (1 - r) / (1 + r)
                             const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
                             float4 dcs;
                             if (V != V_EXACT_SCALAR && P.shade_lds) {
@@ -1257,7 +1283,9 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                             {   // the next segment tests this sphere first (hint_candidate)
                                 const uint32_t sl = thread_slot(wave_base);
                                 lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);  // its geo entry, raytracer.hxx:58
-                                lds_hid[sl] = ib | (dcs.w != 0.f ? 0x80000000u : 0u);
+                                const uint32_t w = __float_as_uint(dcs.w);  // its shortcut word
+                                lds_hid[sl] = ib | (w & kShortcut);
+                                lds_nb[sl] = w;
                             }
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w, xs = dcs.y;

@@ -1,17 +1,20 @@
-"""The isolated-sphere shortcut (rt_kernel.hip hint_candidate, rt_host.cpp isolated_spheres),
-checked as a geometric claim on the CPU with the reference's own binary32 arithmetic.
+"""The walk shortcut of dielectric spheres (rt_kernel.hip hint_candidate, rt_host.cpp
+shortcut_words), checked as a geometric claim on the CPU with the reference's own binary32
+arithmetic.
 
-A lane whose last hit was a dielectric sphere S tests S first; when S is isolated (every other
-clustered sphere's AABB, grown by the walk's box pad for any origin in the ball, is disjoint from
-the ball |p - C|^2 <= fl(fl(r r) 1.0201) plus a rounding margin) and both ends of the lane's
-segment (0, fl(1.002 t_S)] lie in that ball, the kernel skips the cluster walk. The claim: then no
-other clustered sphere's candidate (raytracer.hxx:52-91: near root in (kMIN, kMAX), else far
-root) beats S's in the (t, index) order of closest_hit (raytracer.hxx:94-118). Here rays start
+A lane whose last hit was a dielectric sphere S tests S first; when S has at most two neighbours
+(the other clustered spheres whose AABB, grown by the walk's box pad for any origin in the ball,
+meets the ball |p - C|^2 <= fl(fl(r r) 1.0201) plus a rounding margin) and both ends of the lane's
+segment (0, fl(1.002 t_S)] lie in that ball, the kernel tests the neighbours and skips the cluster
+walk. The claim: then no other clustered sphere's candidate (raytracer.hxx:52-91: near root in
+(kMIN, kMAX), else far root) beats the minimum over S and its neighbours in the (t, index) order
+of closest_hit (raytracer.hxx:94-118). Here rays start
 on (and a few ulp off) the isolated spheres of the reference's huge scene, in every direction
 including near-tangent ones, with |d| from 0.3 to 6; S's candidate and every other sphere's are
 computed op by op in binary32, and every ray that passes the kernel's check is verified.
 (The GPU tests check the kernel's bits with and without the shortcut.)"""
 import numpy as np
+import pytest
 
 import golden_io as G
 
@@ -42,9 +45,9 @@ def _fma32(a, b, c):
     return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
 
 
-def _isolated(C, r, always, kinds, pad0):
-    """rt_host.cpp isolated_spheres, in double."""
-    iso = np.zeros(len(r), dtype=bool)
+def _neighbours(C, r, always, kinds, pad0):
+    """rt_host.cpp shortcut_words, in double: {S: neighbours} for the spheres with a shortcut."""
+    out = {}
     others = np.where(~always)[0]
     ra = np.abs(r.astype(np.float64))
     for S in np.where(kinds == 2)[0]:
@@ -58,12 +61,24 @@ def _isolated(C, r, always, kinds, pad0):
         hi = C[T].astype(np.float64) + ra[T, None] + pad
         x = C[S].astype(np.float64)
         e = np.maximum(np.maximum(lo - x, 0.0), x - hi)
-        iso[S] = bool(((e * e).sum(1) > R * R * (1 + 1e-9)).all())
-    return iso
+        nb = T[~((e * e).sum(1) > R * R * (1 + 1e-9))]
+        if len(nb) <= 2:
+            out[int(S)] = nb
+    return out
 
 
-def test_isolated_sphere_claim_huge_scene():
-    s, m = G.scene("huge")
+def _scene(name):
+    if name == "huge":
+        return G.scene("huge")
+    import test_gpu_parity as P  # the GPU tests' glass-ball scenes (touching and overlapping balls)
+    seed, n, spread = {"glass_sparse": (7, 300, 12.0), "glass_dense": (7, 400, 6.0)}[name]
+    return P._glass_scene(np.random.default_rng(seed), n, spread)
+
+
+@pytest.mark.parametrize("name,min_short,min_nb", [("huge", 150, 30), ("glass_sparse", 150, 50),
+                                                   ("glass_dense", 60, 40)])
+def test_shortcut_claim(name, min_short, min_nb):
+    s, m = _scene(name)
     C = np.ascontiguousarray(s["center"], dtype=np.float32)
     r = np.ascontiguousarray(s["radius"], dtype=np.float32)
     kinds = m["kind"][s["material"]]
@@ -74,13 +89,14 @@ def test_isolated_sphere_claim_huge_scene():
     hi = (C + ra[:, None])[~always].max(0)
     cc, ee = 0.5 * (lo + hi), 0.5 * (hi - lo)
     pad0 = 1e-3 * (np.abs(cc).sum() + ee.sum()) + 1e-6
-    iso = _isolated(C, r, always, kinds, pad0)
-    assert iso.sum() >= 80  # most of the scene's glass balls
+    short = _neighbours(C, r, always, kinds, pad0)
+    n_nb = sum(1 for v in short.values() if len(v))
+    assert len(short) >= min_short and n_nb >= min_nb, (len(short), n_nb)
     others = np.where(~always)[0]
     rng = np.random.default_rng(2024)
     checked = 0
-    for S in np.where(iso)[0]:
-        n = 1500
+    for S, nb in short.items():
+        n = 1000
         u = rng.normal(size=(n, 3))
         u /= np.linalg.norm(u, axis=1, keepdims=True)
         o = (C[S][None, :].astype(np.float64) + ra[S] * u).astype(np.float32)
@@ -105,11 +121,16 @@ def test_isolated_sphere_claim_huge_scene():
         skip = valid & (o2 <= r2k) & (q2 <= r2k)
         if not skip.any():
             continue
-        T = others[others != S]
+        # the shortcut's minimum: S and its neighbours, in (t, index) order
+        own = np.concatenate([[S], nb]).astype(np.int64)
+        t_own = _cand(o[skip], d[skip], C[own], r[own])
+        j = np.lexsort((np.broadcast_to(own, t_own.shape), t_own), axis=1)[:, 0]
+        best_t = t_own[np.arange(len(j)), j]
+        best_i = own[j]
+        T = np.setdiff1d(others, own)
         tT = _cand(o[skip], d[skip], C[T], r[T])
-        # (t, index) order: T beats S if t_T < t_S, or t_T == t_S and T < S
-        beats = (tT < tS[skip, None]) | ((tT == tS[skip, None]) & (T[None, :] < S))
-        assert not beats.any(), f"sphere {S}: {int(beats.sum())} candidates beat the isolated sphere"
+        beats = (tT < best_t[:, None]) | ((tT == best_t[:, None]) & (T[None, :] < best_i[:, None]))
+        assert not beats.any(), f"{name} sphere {S}: {int(beats.sum())} candidates beat the shortcut's minimum"
         checked += int(skip.sum())
-    assert checked > 50000, checked
-    print(f"isolated glass spheres {int(iso.sum())}, rays checked {checked}")
+    assert checked > 20000, checked
+    print(f"{name}: {len(short)} glass spheres with a shortcut ({n_nb} with neighbours), rays checked {checked}")

@@ -81,6 +81,11 @@ def parse():
     ap.add_argument("--rehearse-world", type=int, default=0,
                     help="diagnostic, 1 GPU: render only rank 0's rows of an N-way split (no gather) to "
                          "estimate one rank's frame time at N GPUs; not a bench line")
+    ap.add_argument("--rehearse-rank", type=int, default=0,
+                    help="with --rehearse-world N: which rank's rows (default 0)")
+    ap.add_argument("--rehearse-blocks", action="store_true",
+                    help="with --rehearse-world N: the rank's rows as one contiguous block (H/N rows) instead of "
+                         "every N-th row (A/B of the partition)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process, set before HIP starts (0: leave the environment, "
                          "HIP's default 4): the library runs one render stream fewer than this, 2..7 "
@@ -385,10 +390,12 @@ def main():
     n_spheres = len(arrays[0])
     from raytracinginoneweekend_amd.rowtiles import FrameGather, rank_params
     rehearse = args.rehearse_world if world == 1 and args.rehearse_world > 1 else 0
-    params = rank_params(W, H, spp, rehearse or world, rank, max_depth=depth, seed=args.seed,
-                         scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast",
+    params = rank_params(W, H, spp, rehearse or world, args.rehearse_rank if rehearse else rank, max_depth=depth,
+                         seed=args.seed, scalar_scene=args.variant == "scalar", fast_math=args.variant == "fast",
                          brute_force=args.traversal == "brute", cuda_compat=compat,
                          wavefront=args.variant == "wavefront")
+    if rehearse and args.rehearse_blocks:
+        params.row_offset, params.row_stride = args.rehearse_rank * (H // rehearse), 1
     rows = params.num_rows
     dev = torch.device("cuda", local)
     ds = rt.DeviceScene(arrays, device=local)
@@ -599,7 +606,10 @@ def main():
                 "roofline_achieved": r3(corr["achieved"]), "roofline_frac": round(corr["achieved"] / PEAK_FP32_TFLOPS, 4),
                 "effective_tflops": round(corr["effective_tflops"], 2)}
         if rehearse:
-            rec["rehearsal"] = (f"rank 0 of {rehearse}: rows 0, {rehearse}, ... ({rows} rows), "
+            rr = args.rehearse_rank
+            rows_desc = (f"rows {params.row_offset}..{params.row_offset + rows - 1}" if args.rehearse_blocks
+                         else f"rows {rr}, {rr + rehearse}, ... ({rows} rows)")
+            rec["rehearsal"] = (f"rank {rr} of {rehearse}: {rows_desc}, "
                                 + ("gather's device copies stood in on the caller stream" if args.rehearse_gather
                                    else "no gather") + "; value = "
                                 f"this rank's Mrays/s, x{rehearse} for the ideal {rehearse}-GPU job")

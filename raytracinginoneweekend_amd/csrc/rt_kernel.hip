@@ -388,16 +388,26 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
     for (int k = 0; k < N; ++k) {
         const float4 s = geo[i + k];
         const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;       // raytracer.hxx:55
+        float b, c;
         if (FAST) {  // contracted: 11 VALU per sphere
-            const float b = fmaf(ocx, d.x, fmaf(ocy, d.y, ocz * d.z));
-            const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -s.w)));
-            bq[k] = b;
+            b = fmaf(ocx, d.x, fmaf(ocy, d.y, ocz * d.z));
+            c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -s.w)));
             dq[k] = fmaf(b, b, -(a * c));
         } else {     // the reference's rounding, op by op: 17 VALU per sphere
-            const float b = ocx * d.x + ocy * d.y + ocz * d.z;               // :57
-            const float c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;         // :58
-            bq[k] = b;
+            b = ocx * d.x + ocy * d.y + ocz * d.z;                           // :57
+            c = ocx * ocx + ocy * ocy + ocz * ocz - s.w;                     // :58
             dq[k] = b * b - a * c;                                           // :60
+        }
+        bq[k] = b;
+        if (N == 1) {
+            // The always-tested spheres (the ground): a ray leaving the sphere (b > 0) from
+            // outside it (c >= 0) has no candidate unless rounding makes the far root reach
+            // kMIN: with a c >= 0 the discriminant is at most RN(b^2), so its correctly rounded
+            // root q is at most b + ulp(b), the near root is negative and the far root
+            // RN((q - b) / a) <= RN(ulp(b) / a) < kMIN when b 2^-22 < kMIN a. Such lanes need
+            // no root work: their discriminant is set to -1 (no candidate, as computed), and a
+            // wave of them (upward rays from above the ground: the sky) skips it.
+            if (b > 0.f && c >= 0.f && b * 0x1p-22f < RT_TMIN * a) dq[k] = -1.f;
         }
     }
     // pairwise max tree (NaN never wins)

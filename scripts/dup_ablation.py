@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Timing-only builds (wrong nothing: same paths, same bits) that run one part of the render
+loop twice on an opaque copy of its inputs, so the frame-time difference is that part's marginal
+cost.  python scripts/dup_ablation.py  ->  scripts/_abl/dup_<part>/librt_mi355x.so"""
+import os
+import shutil
+import subprocess
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "raytracinginoneweekend_amd", "csrc")
+K = "rt_kernel.hip"
+PATCHES = {
+    "reject": ("            const f3 r = random_in_unit_sphere_capped<STATS>(st, inc, got, dbg);\n",
+               "            {\n"
+               "                uint64_t st2 = st;\n"
+               "                uint32_t lo2 = (uint32_t)st2, hi2 = (uint32_t)(st2 >> 32);\n"
+               "                asm volatile(\"\" : \"+v\"(lo2), \"+v\"(hi2));\n"
+               "                st2 = ((uint64_t)hi2 << 32) | lo2;\n"
+               "                bool g2;\n"
+               "                const f3 r2 = random_in_unit_sphere_capped<STATS>(st2, inc, g2, dbg);\n"
+               "                asm volatile(\"\" ::\"v\"(r2.x), \"v\"(r2.y), \"v\"(r2.z), \"v\"((uint32_t)st2), \"v\"((uint32_t)g2));\n"
+               "            }\n"),
+    "hit": ("            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);\n",
+            "            {\n"
+            "                f3 o2 = o;\n"
+            "                asm volatile(\"\" : \"+v\"(o2.x));\n"
+            "                const Hit h2 = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o2, d, rd, dbg, wt, walk, wm, tw, key0);\n"
+            "                asm volatile(\"\" ::\"v\"((uint32_t)h2.key), \"v\"((uint32_t)(h2.key >> 32)));\n"
+            "            }\n"),
+    "boxes2": ("            const bool bs = box_pass(rb, s0, s1, t_lo, h.t() * 1.002f);\n",
+               "            {\n"
+               "                float4 s0b = s0;\n"
+               "                asm volatile(\"\" : \"+v\"(s0b.x));\n"
+               "                const bool bs2 = box_pass(rb, s0b, s1, t_lo, h.t() * 1.002f);\n"
+               "                asm volatile(\"\" ::\"v\"((uint32_t)bs2));\n"
+               "            }\n"),
+    "ground": ("    run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);\n",
+               "    {\n"
+               "        f3 o2 = o;\n"
+               "        asm volatile(\"\" : \"+v\"(o2.x));\n"
+               "        Hit h2{key0};\n"
+               "        run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o2, d, rd, h2, dbg);\n"
+               "        asm volatile(\"\" ::\"v\"((uint32_t)h2.key), \"v\"((uint32_t)(h2.key >> 32)));\n"
+               "    }\n"),
+}
+FLAGS = ["-std=c++17", "-O3", "-fno-slp-vectorize", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
+         "-fPIC"]
+for name, (anchor, extra) in PATCHES.items():
+    out = os.path.join(REPO, "scripts", "_abl", "dup_" + name)
+    src = os.path.join(out, "src")
+    shutil.rmtree(out, ignore_errors=True)
+    os.makedirs(src)
+    for f in ("rt_kernel.hip", "rt_host.cpp", "rt_device.h"):
+        shutil.copy(os.path.join(SRC, f), src)
+    os.makedirs(os.path.join(out, "include"), exist_ok=True)
+    text = open(os.path.join(src, K)).read()
+    assert text.count(anchor) == 1, name
+    text = text.replace(anchor, anchor + extra if name != "ground" else extra + anchor)
+    open(os.path.join(src, K), "w").write(text)
+    inc = ["-I", os.path.join(REPO, "include")]
+    r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *inc, "-Rpass-analysis=kernel-resource-usage", "-c",
+                        os.path.join(src, K), "-o", os.path.join(out, "k.o")], check=True, capture_output=True, text=True)
+    lines = r.stderr.splitlines()
+    i = next(j for j, line in enumerate(lines) if "render_kernelILi0ELi7ELb0ELb0E" in line)
+    print(name, " ".join(x.split(":")[-1].strip().split(" [")[0] for x in lines[i + 1:i + 9]
+                         if "GPRs" in x or "Occupancy" in x))
+    # the host side is unchanged: the product build's object (make -C raytracinginoneweekend_amd/csrc)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                    os.path.join(out, "librt_mi355x.so"), os.path.join(out, "k.o"), os.path.join(SRC, "_obj", "rt_host.o"),
+                    "-Wl,--no-undefined"], check=True)
+    shutil.rmtree(src)
+    print("built", out)

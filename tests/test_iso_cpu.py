@@ -134,3 +134,36 @@ def test_shortcut_claim(name, min_short, min_nb):
         checked += int(skip.sum())
     assert checked > 20000, checked
     print(f"{name}: {len(short)} glass spheres with a shortcut ({n_nb} with neighbours), rays checked {checked}")
+
+
+@pytest.mark.parametrize("C,r", [((0.0, -1000.0, 0.0), 1000.0), ((1.5, 0.2, -3.0), 0.2), ((0.0, 1.0, 0.0), -0.95)])
+def test_leaving_ray_gate_claim(C, r):
+    """test_block8's gate for the always-tested spheres: a ray with b > 0 and c >= 0 (computed)
+    and b 2^-22 < kMIN a has no candidate (raytracer.hxx:52-91) — checked op by op in binary32
+    on rays from (and a few ulp around) the sphere's surface and from afar, near-tangent ones
+    and ones with tiny |d| included."""
+    rng = np.random.default_rng(7)
+    Cf = np.array(C, dtype=np.float32)
+    rf = np.float32(r)
+    n = 400000
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    dist = np.where(rng.random(n) < 0.7, abs(r), abs(r) * rng.uniform(1.0, 3.0, n))
+    o = (Cf.astype(np.float64) + dist[:, None] * u).astype(np.float32)
+    o = (o.view(np.int32) + rng.integers(-4, 5, size=o.shape).astype(np.int32)).view(np.float32)
+    v = rng.normal(size=(n, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    tang = v - (v * u).sum(1, keepdims=True) * u
+    tang /= np.linalg.norm(tang, axis=1, keepdims=True)
+    k = n // 2
+    v[:k] = tang[:k] + rng.uniform(-1e-4, 1e-2, (k, 1)) * u[:k]
+    d = (v * np.exp(rng.uniform(np.log(1e-4), np.log(8.0), (n, 1)))).astype(np.float32)
+    ocx, ocy, ocz = (o[:, j] - Cf[j] for j in range(3))
+    dx, dy, dz = d[:, 0], d[:, 1], d[:, 2]
+    a = (dx * dx + dy * dy) + dz * dz
+    b = (ocx * dx + ocy * dy) + ocz * dz
+    c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - rf * rf
+    gate = (b > 0) & (c >= 0) & (b * np.float32(2.0 ** -22) < KMIN * a)
+    assert gate.sum() > n // 10
+    t = _cand(o[gate], d[gate], Cf[None, :], np.array([rf]))[:, 0]
+    assert np.isinf(t).all(), f"{int(np.isfinite(t).sum())} gated rays have a candidate"

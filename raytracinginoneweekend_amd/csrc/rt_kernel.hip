@@ -907,14 +907,15 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                     // region (a wave starts on its workgroup's region)
                     if (lane == 0) c = atomicAdd(P.deep.ctr + q * kQueueStride + kDeepDeal, 1u);
                     c = __builtin_amdgcn_readfirstlane(c);
-                    const uint32_t nq = min(P.deep.ctr[q * kQueueStride + kDeepCount], P.deep.rcap);
+                    const uint32_t nq = __builtin_amdgcn_readfirstlane(
+                        min(P.deep.ctr[q * kQueueStride + kDeepCount], P.deep.rcap));
                     if (c >= (nq + 63u) / 64u) {
                         q = (q + 1u) & 7u;
                         if (++q_tried == 8u) exhausted = true;
                         continue;
                     }
-                    cnext = q * P.deep.rcap + 64u * c;
-                    cend = q * P.deep.rcap + min(64u * c + 64u, nq);
+                    cnext = __builtin_amdgcn_readfirstlane(q * P.deep.rcap + 64u * c);
+                    cend = __builtin_amdgcn_readfirstlane(q * P.deep.rcap + min(64u * c + 64u, nq));
                 } else {
                 if (lane == 0) c = atomicAdd(P.queue_ctr + q * kQueueStride, 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
@@ -933,14 +934,14 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                         const uint64_t g = (uint64_t)floorf((float)B * (1.f - x)) + 2ull * t;
                         return g < B ? (uint32_t)g : B;
                     };
-                    const uint32_t s0 = S(c);
+                    const uint32_t s0 = __builtin_amdgcn_readfirstlane(S(c));
                     if (s0 >= B) {
                         q = (q + 1u) & 7u;
                         if (++q_tried == 8u) exhausted = true;
                         continue;
                     }
                     cnext = 64u * (qb0 + s0);
-                    cend = min(64u * (qb0 + S(c + 1u)), P.n_items);
+                    cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), P.n_items));
                 } else {
                 const uint64_t chunk = (uint64_t)q + 8ull * c;
                 if (chunk >= P.n_chunks) {

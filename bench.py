@@ -188,7 +188,16 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-TIMED_KERNEL = "_ZN2rt13render_kernelILi0ELi7ELb0ELb0EEEvNS_7KParamsE"  # rt::render_kernel<0, 7, false, false>
+# the timed kernels: rt::render_kernel<0, 7, false, false> (main launch) and
+# rt::render_deep_kernel<0, false, false> (the deep launch of a split pass)
+TIMED_KERNEL = ("_ZN2rt13render_kernelILi0ELi7ELb0ELb0EEEvNS_7KParamsE",
+                "_ZN2rt18render_deep_kernelILi0ELb0ELb0EEEvNS_7KParamsE")
+TIMED_KERNEL_NAMES = "render_kernel<0, 7, false, false>,render_deep_kernel<0, false, false>"
+
+
+def hashlib_sha256(b):
+    import hashlib
+    return hashlib.sha256(b).hexdigest()
 
 
 def _elf_sections(b):
@@ -201,9 +210,15 @@ def _elf_sections(b):
 
 
 def kernel_sha256(symbol=TIMED_KERNEL):
-    """sha256 of one kernel's machine code and kernel descriptor in the gfx950 code objects of
-    the loaded library (PMC summaries are stamped with it, so host-side or other-instantiation
-    changes do not invalidate them); None if the symbol is not found."""
+    """sha256 of the machine code and kernel descriptors of one kernel (a symbol) or several (a
+    tuple) in the gfx950 code objects of the loaded library (PMC summaries are stamped with it,
+    so host-side or other-instantiation changes do not invalidate them); None if a symbol is
+    not found."""
+    if isinstance(symbol, (tuple, list)):
+        parts = [kernel_sha256(x) for x in symbol]
+        if None in parts:
+            return None
+        return hashlib_sha256("".join(parts).encode())
     import hashlib
     import struct
     from raytracinginoneweekend_amd import _lib
@@ -579,7 +594,7 @@ def main():
         }
         v = {"exact": 0, "scalar": 1, "fast": 2, "wavefront": 0}[args.variant]
         cull = 0 if args.traversal == "brute" or v == 1 else 7
-        kname = f"render_kernel<{v}, {cull}, false, false>"
+        kname = TIMED_KERNEL_NAMES if (v, cull) == (0, 7) else f"render_kernel<{v}, {cull}, false, false>"
         pmc, status = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
                                                    "traversal": args.traversal, "n_gpus": world})
         if args.variant == "wavefront":  # other kernels did the work: no render_kernel PMC

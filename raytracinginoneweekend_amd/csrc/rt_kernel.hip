@@ -780,8 +780,11 @@ __device__ __forceinline__ float4 gld4(const float4 *p, uint32_t i)
 #endif
 template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_PER_SIMD;
-template <int V, int CULL, bool STATS, bool COUNT>
-__global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kernel(const KParams p)
+// The render loop; DEEP: the deep launch of a split pass (KParams::deep_mode),
+// whose items are queued paths (no sample starts, no lens draws, no split) — its own
+// instantiation, render_deep_kernel, so neither launch carries the other's code.
+template <int V, int CULL, bool STATS, bool COUNT, bool DEEP>
+__device__ __forceinline__ void render_body(const KParams &p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
     // Scene blob -> LDS (or read in place from global for the scalar-cache A/B variant):
@@ -826,7 +829,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     // the deep launch's waves issue ahead of other launches' waves (KParams::deep_prio): each of
     // its paths is a chain of ~56 dependent iterations, which beside other renders' waves on the
     // same SIMD would take ~7x as long
-    if (p.deep_mode && p.deep_prio) __builtin_amdgcn_s_setprio(3);
+    if (DEEP && p.deep_prio) __builtin_amdgcn_s_setprio(3);
     // wave-uniform cursor over the item space (the deep launch: over the queued paths)
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
     uint32_t cnext = 0, cend = 0;
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
             RT_EV(EV_REFILL_TRIP);
             if (cnext >= cend) {
                 uint32_t c = 0;
-                if (P.deep_mode) {
+                if constexpr (DEEP) {
                     // the deep launch: 64 queued paths per grab from region q, then the next
                     // region (a wave starts on its workgroup's region)
                     if (lane == 0) c = atomicAdd(P.deep.ctr + q * kQueueStride + kDeepDeal, 1u);
@@ -966,7 +969,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (!alive && rank < avail) {
                 const uint32_t I = cnext + rank;
-                if (P.deep_mode) {
+                if constexpr (DEEP) {
                     // a queued path resumes where the main launch left it: the ray of its next
                     // segment, attenuation, data stream and segment count; ls = 0 and pix = the
                     // slot index address the same slot
@@ -1041,7 +1044,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         // waits for its unluckiest lane's whole run (mean 1.91 attempts, ~6.9 for the worst of
         // 64 lanes), and every stream still sees the same draws in the same order.
         bool defer = false;
-        const bool lens = fresh || pend_lens;
+        const bool lens = !DEEP && (fresh || pend_lens);
         if (lens || pend) {
             const uint64_t inc = lens ? (((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo) : inc_data;
             if (pend_lens) {
@@ -1119,7 +1122,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
         // region, trace paths of the same few spheres, whose segments reach the same few
         // clusters (8 counters on separate lines spread the appends). A path that finds its
         // region full stays in this launch.
-        if (P.deep_depth) {
+        if (!DEEP && P.deep_depth) {
             const bool dv = alive && !defer && depth == P.deep_depth;
             if (ballot(dv)) {
                 uint32_t j = ~0u, r = 0;
@@ -1370,6 +1373,18 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
                                 min(dbg_refills, 65535u);
         }
     }
+}
+
+template <int V, int CULL, bool STATS, bool COUNT>
+__global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kernel(const KParams p)
+{
+    render_body<V, CULL, STATS, COUNT, false>(p);
+}
+// the deep launch of a split pass (culled scenes only)
+template <int V, bool STATS, bool COUNT>
+__global__ __launch_bounds__(256, (kMinWaves<V, 7, STATS>)) void render_deep_kernel(const KParams p)
+{
+    render_body<V, 7, STATS, COUNT, true>(p);
 }
 
 // ---- the reference's CUDA variant (RT_FLAG_CUDA_COMPAT) -----------------------------------
@@ -1870,9 +1885,23 @@ static const void *render_ptr(int variant, int cull, bool count)
     return count ? render_ptr_c<true>(variant, cull) : render_ptr_c<false>(variant, cull);
 }
 
+template <bool COUNT> static const void *render_deep_ptr_c(int variant)
+{
+    switch (variant) {
+    case V_EXACT_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_EXACT_LDS, false, COUNT>);
+    case V_FAST_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_FAST_LDS, false, COUNT>);
+    case V_STATS_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_EXACT_LDS, true, true>);
+    default: return nullptr;
+    }
+}
+
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream)
 {
-    const void *fn = render_ptr(variant, cull, p.segments != nullptr);
+    // the deep launch (deep_mode != 0) exists for culled scenes only
+    const bool count = p.segments != nullptr;
+    const void *fn = p.deep_mode ? (cull == 7 ? (count ? render_deep_ptr_c<true>(variant) : render_deep_ptr_c<false>(variant))
+                                              : nullptr)
+                                 : render_ptr(variant, cull, count);
     if (!fn) return hipErrorInvalidValue;
     const size_t lds = (size_t)p.lds_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};

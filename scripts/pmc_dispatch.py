@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """rocprofv3 --pmc passes (pmc_round.sh layout: <root>/p*/run_counter_collection.csv and
-run_kernel_trace.csv) split per render_kernel dispatch into the main launches and the deep
-launches of split passes: a frame's deep launch is the render dispatch that follows its main
-launch on the same queue with the same grid; here they are told apart by duration (a deep launch
-is the shorter one, below --split-ms).    python scripts/pmc_dispatch.py <root> [--split-ms 1.8]
+run_kernel_trace.csv) split into the main launches (render_kernel) and the deep launches of
+split passes (render_deep_kernel; builds before it had one kernel for both, told apart here by
+duration: the deep launch is the shorter one, below --split-ms).
+    python scripts/pmc_dispatch.py <root> [--split-ms 1.8]
 """
 import argparse
 import csv
@@ -17,19 +17,25 @@ ap.add_argument("--split-ms", type=float, default=1.8)
 a = ap.parse_args()
 groups = {"main": defaultdict(list), "deep": defaultdict(list)}
 for d in sorted(x for x in glob.glob(os.path.join(a.root, "p*")) if os.path.isdir(x)):
-    dur = {}
+    dur, deep = {}, set()
     for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))):
-        if "render_kernel" in r["Kernel_Name"]:
+        if "render_kernel" in r["Kernel_Name"] or "render_deep_kernel" in r["Kernel_Name"]:
             dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            if "render_deep_kernel" in r["Kernel_Name"]:
+                deep.add(r["Dispatch_Id"])
     per = defaultdict(float)
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if "render_kernel" in r["Kernel_Name"]:
+        if "render_kernel" in r["Kernel_Name"] or "render_deep_kernel" in r["Kernel_Name"]:
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+    def kind(di):
+        if deep:
+            return "deep" if di in deep else "main"
+        return "main" if dur[di] >= a.split_ms else "deep"
     for (di, c), v in per.items():
         if di in dur:
-            groups["main" if dur[di] >= a.split_ms else "deep"][c].append(v)
+            groups[kind(di)][c].append(v)
     for di, t in dur.items():
-        groups["main" if t >= a.split_ms else "deep"]["duration_ms"].append(t)
+        groups[kind(di)]["duration_ms"].append(t)
 for g, vals in groups.items():
     n = len(vals.get("duration_ms", []))
     print(f"== {g} launches (n={n} dispatches over the passes)")

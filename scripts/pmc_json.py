@@ -2,7 +2,7 @@
 """Condense rocprofv3 --pmc passes of bench.py into the JSON bench.py reads for roofline.traffic.
 
     python scripts/pmc_json.py <pmc dir with p*/run_counter_collection.csv> <out.json> \
-        [--kernel 'render_kernel<0, 7, false, false>'] [--config c3] [--camera reference]
+        [--kernel 'render_kernel<0, 7, false, false>,render_deep_kernel<0, false, false>'] [--config c3]
 
 Per frame (the kernel's dispatches of a frame summed, mean over frames and passes):
   hbm_bytes_per_frame  = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE counts half of the
@@ -23,34 +23,42 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ap = argparse.ArgumentParser()
 ap.add_argument("root")
 ap.add_argument("out")
-ap.add_argument("--kernel", default="render_kernel<0, 7, false, false>")
+ap.add_argument("--kernel", default="render_kernel<0, 7, false, false>,render_deep_kernel<0, false, false>",
+                help="comma-separated kernel names; the first one's dispatches count the frames")
 ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")
 ap.add_argument("--traversal", default="cull")
 ap.add_argument("--simds", type=int, default=1024)  # 256 CUs x 4 SIMDs
-ap.add_argument("--dispatches-per-frame", type=int, default=2)
 a = ap.parse_args()
+names = [k.strip() for k in a.kernel.split(",") if k.strip()]
 
-# Per frame: every dispatch of the kernel in a pass summed and divided by the frames, i.e. the
-# dispatches / --dispatches-per-frame (2 with the deep-path split on a one-pass frame such as
-# config 3: the main launch and the deep launch; 1 without it).
+
+def which(kernel_name):
+    return next((i for i, k in enumerate(names) if k in kernel_name), None)
+
+
+# Per frame: every dispatch of the kernels in a pass summed and divided by the frames, i.e. the
+# dispatches of the first kernel (one main launch per frame for a one-pass frame such as config
+# 3; its deep launch is the second kernel's dispatch)
 vals = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_counter_collection.csv"))):
     per = defaultdict(float)
-    disp = set()
+    frames = set()
     for r in csv.DictReader(open(f)):
-        if a.kernel not in r["Kernel_Name"]:
+        i = which(r["Kernel_Name"])
+        if i is None:
             continue
-        disp.add(r["Dispatch_Id"])
+        if i == 0:
+            frames.add(r["Dispatch_Id"])
         per[r["Counter_Name"]] += float(r["Counter_Value"])
     for c, v in per.items():
-        vals[c].append(v * a.dispatches_per_frame / len(disp))
+        vals[c].append(v / len(frames))
 dur = []
 for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_kernel_trace.csv"))):
-    ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-          for r in csv.DictReader(open(f)) if a.kernel in r["Kernel_Name"]]
-    if ds:
-        dur.append(sum(ds) * a.dispatches_per_frame / len(ds))
+    rows = [r for r in csv.DictReader(open(f)) if which(r["Kernel_Name"]) is not None]
+    n = sum(1 for r in rows if which(r["Kernel_Name"]) == 0)
+    if n:
+        dur.append(sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rows) / n)
 m = {c: sum(v) / len(v) for c, v in vals.items()}
 need = ["FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]
 missing = [c for c in need if c not in m]
@@ -61,7 +69,7 @@ from bench import WORKLOAD, kernel_sha256, lib_sha256  # noqa: E402
 t = sum(dur) / len(dur)
 cycles = m["GRBM_GUI_ACTIVE"] / 8.0
 rec = {
-    "kernel": a.kernel,
+    "kernel": ",".join(names),
     # the build these counters describe: bench.py uses them only for the same library
     "kernel_sha256": kernel_sha256(),
     "lib_sha256": lib_sha256(),
@@ -69,7 +77,6 @@ rec = {
     # per frame: the kernel's dispatches of one frame (durations summed: a span of overlapping
     # launches when frames are in flight)
     "kernel_ms_per_frame": round(t * 1e3, 4),
-    "dispatches_per_frame": a.dispatches_per_frame,
     "clock_ghz": round(cycles / t / 1e9, 3),
     "hbm_bytes_per_frame": int(2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024),
     "fetch_bytes_corrected": int(2 * m["FETCH_SIZE"] * 1024),

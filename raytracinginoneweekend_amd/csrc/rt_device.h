@@ -23,9 +23,11 @@ namespace rt {
 // Per-render constants used only where a sample or an item starts (the kernel re-reads them
 // from the kernarg segment at each use; see render_kernel).
 // Exact unsigned division by a per-render invariant d (Granlund-Montgomery, "round-up with
-// add"): q = (t + ((n - t) >> 1)) >> (l - 1), t = mulhi(n, m), for every 32-bit n.
+// add"): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(n, m), for every 32-bit n; d >= 2: s1 = 1,
+// s2 = ceil(log2 d) - 1, m = floor(2^32 (2^ceil(log2 d) - d) / d) + 1; d = 1: m = s1 = s2 = 0
+// (t = 0, q = n), so no branch.
 struct UDiv {
-    uint32_t m, l;   // l = ceil(log2 d) (>= 1), m = floor(2^32 (2^l - d) / d) + 1; d = 1: l = 0
+    uint32_t m, s1, s2;
 };
 
 struct FrameConsts {

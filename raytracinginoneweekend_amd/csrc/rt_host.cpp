@@ -684,11 +684,12 @@ int check_params(const rt_params *p)
 
 rt::UDiv make_udiv(uint32_t d)
 {
-    rt::UDiv r{0, 0};
-    if (d <= 1) return r;  // d = 1: identity (l = 0)
+    rt::UDiv r{0, 0, 0};
+    if (d <= 1) return r;  // d = 1: identity (t = 0, no shifts)
     uint32_t l = 0;
     while ((1ull << l) < d) ++l;
-    r.l = l;
+    r.s1 = 1;
+    r.s2 = l - 1;
     r.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1);
     return r;
 }

@@ -213,11 +213,11 @@ __device__ __forceinline__ float schlick_x(float xf, float c)
 __device__ __forceinline__ float schlick(float ri, float c) { return schlick_x((1.f - ri) / (1.f + ri), c); }
 
 // ---- work decomposition ----------------------------------------------------------------
-__device__ __forceinline__ uint32_t udiv(uint32_t n, uint32_t m, uint32_t l)
+template <class UD>
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const UD &u)
 {
-    if (l == 0) return n;
-    const uint32_t t = __umulhi(n, m);
-    return (t + ((n - t) >> 1)) >> (l - 1);
+    const uint32_t t = __umulhi(n, u.m);
+    return (t + ((n - t) >> u.s1)) >> u.s2;
 }
 
 template <class FC>
@@ -227,13 +227,13 @@ __device__ __forceinline__ void pixel_of(const FC &fc, uint32_t i, uint32_t &x, 
     const uint32_t tiled_px = tiled_rows * W;
     if (i < tiled_px) {
         uint32_t t = i >> 6, w = i & 63u;
-        uint32_t ty = udiv(t, fc.div_tiles_x.m, fc.div_tiles_x.l), tx = t - ty * tiles_x;
+        uint32_t ty = udiv(t, fc.div_tiles_x), tx = t - ty * tiles_x;
         const uint32_t lw = fc.tile_lw;
         x = (tx << lw) + (w & ((1u << lw) - 1u));
         rr = (ty << (6u - lw)) + (w >> lw);
     } else {
         uint32_t j = i - tiled_px;
-        rr = udiv(j, fc.div_W.m, fc.div_W.l);
+        rr = udiv(j, fc.div_W);
         x = j - rr * W;
         rr += tiled_rows;
     }
@@ -994,7 +994,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     }
                     lds_hid[sl] = hid;
                 } else {
-                    ls = udiv(I, fc->div_n_pixels.m, fc->div_n_pixels.l);
+                    ls = udiv(I, fc->div_n_pixels);
                     pix = I - ls * fc->n_pixels;
                     alive = fresh = true;
                 }
@@ -1024,11 +1024,19 @@ __device__ __forceinline__ void render_body(const KParams &p)
             rng = km + inc_data * (kPcgMul + 1u);
             rc = km + inc_cam * (kPcgMul + 1u);
             const float fW = fc->fW, fH = fc->fH, rW = fc->rW, rH = fc->rH;
-            const bool fw = fc->div_fast & 1u, fh = fc->div_fast & 2u;
-            const float u = div_const((float)px, fW, rW, fw);
-            const float v = div_const((float)py, fH, rH, fh);
-            uu = u + div_const(canonical(rng, inc_data), fW, rW, fw);
-            vv = v + div_const(canonical(rng, inc_data), fH, rH, fh);
+            const uint32_t df = fc->div_fast;
+            const float xu = canonical(rng, inc_data);  // the u jitter's draw, then v's
+            const float xv = canonical(rng, inc_data);
+            if (df == 3u) {
+                // both divisors take the checked short form (the common case): one uniform
+                // branch for the four divisions instead of one per division
+                uu = div_const((float)px, fW, rW, true) + div_const(xu, fW, rW, true);
+                vv = div_const((float)py, fH, rH, true) + div_const(xv, fH, rH, true);
+            } else {
+                const bool fw = df & 1u, fh = df & 2u;
+                uu = div_const((float)px, fW, rW, fw) + div_const(xu, fW, rW, fw);
+                vv = div_const((float)py, fH, rH, fh) + div_const(xv, fH, rH, fh);
+            }
             att = mk(1.f, 1.f, 1.f);
             depth = 0;
             lds_hid[thread_slot(wave_base)] = ~0u;
@@ -1661,7 +1669,7 @@ __global__ __launch_bounds__(256) void wave_gen_kernel(const KWave w)
     const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
     if (gid >= w.n_chunk) return;
     const uint32_t I = w.item_begin + gid;
-    const uint32_t ls = udiv(I, fc.div_n_pixels.m, fc.div_n_pixels.l);
+    const uint32_t ls = udiv(I, fc.div_n_pixels);
     const uint32_t pix = I - ls * fc.n_pixels;
     uint32_t px, rr;
     pixel_of(fc, pix, px, rr);

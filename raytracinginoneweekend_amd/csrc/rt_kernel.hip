@@ -316,7 +316,7 @@ __device__ __forceinline__ RayDiv ray_div(float a, uint64_t active, uint32_t fas
     const float y0 = __builtin_amdgcn_rcpf(a);
     const float y = fmaf(fmaf(-a, y0, 1.f), y0, y0);
     const uint64_t ok = ballot(a >= 0x1p-40f) & ballot(a <= 0x1p40f);  // NaN: neither
-    return {a, y, (fast_roots != 0u && !(active & ~ok)) ? 1u : 0u};
+    return {a, y, (uint32_t)__builtin_amdgcn_readfirstlane((fast_roots != 0u && !(active & ~ok)) ? 1u : 0u)};
 }
 // n / a: the IEEE sequence (v_div_scale, rcp + refinement, two FMA corrections, v_div_fmas,
 // v_div_fixup) with no scaling and no special value, i.e. its two corrections
@@ -343,7 +343,7 @@ __device__ __forceinline__ float sqrt_scaled(float x)
 // sphere loops as a lane predicate and rebuilds its negation per use with two VALU operations
 __device__ __forceinline__ bool fast_div(const RayDiv &r)
 {
-    uint32_t f = __builtin_amdgcn_readfirstlane(r.fd);
+    uint32_t f = r.fd;  // uniform by construction (ray_div): an SGPR, no readfirstlane here
     asm volatile("" : "+s"(f));
     return f != 0u;
 }

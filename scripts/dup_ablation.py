@@ -43,9 +43,38 @@ PATCHES = {
                "        asm volatile(\"\" ::\"v\"((uint32_t)h2.key), \"v\"((uint32_t)(h2.key >> 32)));\n"
                "    }\n"),
 }
+PATCHES.update({
+    "members_t": ("        members_transposed<FAST, STATS>(geo, sidx, start, cnt, M, req, tw, o, d, rd, h, dbg);\n",
+                  "        {\n"
+                  "            f3 o2 = o;\n"
+                  "            asm volatile(\"\" : \"+v\"(o2.x));\n"
+                  "            Hit h2 = h;\n"
+                  "            members_transposed<FAST, STATS>(geo, sidx, start, cnt, M, req, tw, o2, d, rd, h2, dbg);\n"
+                  "            asm volatile(\"\" ::\"v\"((uint32_t)h2.key), \"v\"((uint32_t)(h2.key >> 32)));\n"
+                  "        }\n"),
+    "members_l": ("        run_members<FAST, STATS>(geo, sidx, start, cnt, o, d, rd, h, dbg);\n",
+                  "        {\n"
+                  "            f3 o2 = o;\n"
+                  "            asm volatile(\"\" : \"+v\"(o2.x));\n"
+                  "            Hit h2 = h;\n"
+                  "            run_members<FAST, STATS>(geo, sidx, start, cnt, o2, d, rd, h2, dbg);\n"
+                  "            asm volatile(\"\" ::\"v\"((uint32_t)h2.key), \"v\"((uint32_t)(h2.key >> 32)));\n"
+                  "        }\n"),
+    "refract": ("                            const f3 refr = refract(ud, outward, ri);\n",
+                "                            {\n"
+                "                                f3 u2 = ud;\n"
+                "                                asm volatile(\"\" : \"+v\"(u2.x));\n"
+                "                                const f3 r2 = refract(u2, outward, ri);\n"
+                "                                const float p2 = schlick_x(xs, cosv + u2.x * 0.f);\n"
+                "                                asm volatile(\"\" ::\"v\"(r2.x), \"v\"(r2.y), \"v\"(r2.z), \"v\"(p2));\n"
+                "                            }\n"),
+})
+ONLY = os.environ.get("DUP_ONLY", "").split(",") if os.environ.get("DUP_ONLY") else None
 FLAGS = ["-std=c++17", "-O3", "-fno-slp-vectorize", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
          "-fPIC"]
 for name, (anchor, extra) in PATCHES.items():
+    if ONLY and name not in ONLY:
+        continue
     out = os.path.join(REPO, "scripts", "_abl", "dup_" + name)
     src = os.path.join(out, "src")
     shutil.rmtree(out, ignore_errors=True)
@@ -54,8 +83,9 @@ for name, (anchor, extra) in PATCHES.items():
         shutil.copy(os.path.join(SRC, f), src)
     os.makedirs(os.path.join(out, "include"), exist_ok=True)
     text = open(os.path.join(src, K)).read()
-    assert text.count(anchor) == 1, name
-    text = text.replace(anchor, anchor + extra if name != "ground" else extra + anchor)
+    assert text.count(anchor) >= 1, name
+    # the render loop's copy (the first occurrence; the wavefront kernel has its own)
+    text = text.replace(anchor, anchor + extra if name != "ground" else extra + anchor, 1)
     open(os.path.join(src, K), "w").write(text)
     inc = ["-I", os.path.join(REPO, "include")]
     r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *inc, "-Rpass-analysis=kernel-resource-usage", "-c",

@@ -192,7 +192,7 @@ def lib_sha256():
 # rt::render_deep_kernel<0, false, false> (the deep launch of a split pass)
 TIMED_KERNEL = ("_ZN2rt13render_kernelILi0ELi7ELb0ELb0EEEvNS_7KParamsE",
                 "_ZN2rt18render_deep_kernelILi0ELb0ELb0EEEvNS_7KParamsE")
-TIMED_KERNEL_NAMES = "render_kernel<0, 7, false, false>,render_deep_kernel<0, false, false>"
+TIMED_KERNEL_NAMES = "render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false>"
 
 
 def hashlib_sha256(b):

@@ -2,7 +2,7 @@
 """Condense rocprofv3 --pmc passes of bench.py into the JSON bench.py reads for roofline.traffic.
 
     python scripts/pmc_json.py <pmc dir with p*/run_counter_collection.csv> <out.json> \
-        [--kernel 'render_kernel<0, 7, false, false>,render_deep_kernel<0, false, false>'] [--config c3]
+        [--kernel 'render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false>'] [--config c3]
 
 Per frame (the kernel's dispatches of a frame summed, mean over frames and passes):
   hbm_bytes_per_frame  = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE counts half of the
@@ -23,14 +23,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ap = argparse.ArgumentParser()
 ap.add_argument("root")
 ap.add_argument("out")
-ap.add_argument("--kernel", default="render_kernel<0, 7, false, false>,render_deep_kernel<0, false, false>",
-                help="comma-separated kernel names; the first one's dispatches count the frames")
+ap.add_argument("--kernel", default="render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false>",
+                help="kernel names joined by ' + '; the first one's dispatches count the frames")
 ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")
 ap.add_argument("--traversal", default="cull")
 ap.add_argument("--simds", type=int, default=1024)  # 256 CUs x 4 SIMDs
 a = ap.parse_args()
-names = [k.strip() for k in a.kernel.split(",") if k.strip()]
+names = [k.strip() for k in a.kernel.split(" + ") if k.strip()]
 
 
 def which(kernel_name):
@@ -69,7 +69,7 @@ from bench import WORKLOAD, kernel_sha256, lib_sha256  # noqa: E402
 t = sum(dur) / len(dur)
 cycles = m["GRBM_GUI_ACTIVE"] / 8.0
 rec = {
-    "kernel": ",".join(names),
+    "kernel": " + ".join(names),
     # the build these counters describe: bench.py uses them only for the same library
     "kernel_sha256": kernel_sha256(),
     "lib_sha256": lib_sha256(),

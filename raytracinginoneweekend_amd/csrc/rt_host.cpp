@@ -113,12 +113,15 @@ uint32_t chunk_items()
 // stream: K = 6 3.93 ms/frame with single-frame latency unchanged (5.3-5.4 ms); K = 4
 // 3.89-3.92 but 6.2 ms latency; the fixed scheme (RT_SCHED=fixed: RT_CHUNK_ITEMS chunks, the
 // last RT_TAIL_PCT % in 64s) 4.39 ms at 512/8%, 3.96 at 2048/2% (5.7 ms latency).
-float guided_l2b(uint32_t total_waves)
+// Round 3: a pass issued while no other render runs (a lone frame) deals with K = 12 — its end
+// is not hidden by other launches, and smaller last chunks even it out (config 3 lone frame
+// 3.37-3.45 vs 3.55-3.59 ms, frame stream alike at K = 6/9/12; profiles/r03/ab/guided_k.txt).
+float guided_l2b(uint32_t total_waves, bool in_flight)
 {
     const char *e = std::getenv("RT_SCHED");
     if (e && std::strcmp(e, "fixed") == 0) return 0.f;
     const char *ke = std::getenv("RT_GUIDED_K");
-    const double k = ke && *ke ? std::max(0.25, std::atof(ke)) : 6.0;
+    const double k = ke && *ke ? std::max(0.25, std::atof(ke)) : (in_flight ? 6.0 : 12.0);
     const double wq = std::max(1.0, total_waves / 8.0);
     const double beta = std::max(1.0 - 1.0 / (k * wq), 1.0 / (1 << 20));
     return static_cast<float>(std::log2(beta));
@@ -1354,7 +1357,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
-        k.guided_l2b = guided_l2b(grid * 4u);
+        k.guided_l2b = guided_l2b(grid * 4u, in_flight);
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
         k.deep_depth = 0;
         k.deep_mode = 0;

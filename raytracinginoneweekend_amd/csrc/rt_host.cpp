@@ -910,6 +910,17 @@ int shade_lds_env()
     return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
 }
 
+// the render kernels' static LDS (per-wave transposed-test records 4 x 640 B, per-lane pending
+// normal 256 x 16 B, hint index and shortcut word 2 x 256 x 4 B: 8704 B), with a margin
+constexpr size_t kRenderStaticLds = 12u << 10;
+
+// RT_DEEP_SHADE_LDS=0 keeps the deep launch's shading records in global memory (A/B; default 1)
+bool deep_shade_lds_env()
+{
+    const char *e = std::getenv("RT_DEEP_SHADE_LDS");
+    return !(e && e[0] == '0');
+}
+
 // RT_VERBOSE=1 prints each launch's plan (variant, LDS bytes, occupancy, grid, items) to stderr.
 bool verbose()
 {
@@ -1427,6 +1438,16 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 // same bits)
                 kd.use_root = deep_root_box_env() ? k.use_root : 0u;
                 kd.deep_prio = deep_prio_env();
+                // the shading records in LDS for the deep launch of a pass issued alone: its
+                // paths bounce in glass and shade every segment, and its few busy waves wait on
+                // each global round trip (config 3 single frame: deep launch 0.59 vs 0.65 ms).
+                // Not beside other renders: its larger workgroups then displace theirs (frame
+                // stream 2.69-2.73 vs 2.57-2.59 ms per frame, 8-way share 0.45 vs 0.42)
+                if (deep_shade_lds_env() && !in_flight && variant != rt::V_EXACT_SCALAR && !k.shade_lds &&
+                    static_cast<size_t>(k.blob_units) * 16u + kRenderStaticLds <= sc->max_lds) {
+                    kd.shade_lds = 1u;
+                    kd.lds_units = k.blob_units;
+                }
                 if (variant == rt::V_STATS_LDS && std::getenv("RT_DEBUG_DEEP_ONLY")) {
                     // diagnostics: the counters and events of the deep launch alone
                     RT_HIP(hipMemsetAsync(sc->dbg, 0, 16 * sizeof(unsigned long long), xst));

@@ -362,10 +362,12 @@ __device__ __forceinline__ bool all_lanes_min_abs_ok(f3 n)
 {
     return !ballot(!(fminf(fminf(fabsf(n.x), fabsf(n.y)), fabsf(n.z)) >= 0x1p-100f));
 }
-// the near root (-b - sqrt(disc)) / a and its sqrt, raytracer.hxx:62-63
+// the near root (-b - sqrt(disc)) / a and its sqrt, raytracer.hxx:62-63; FD: 1 the short forms
+// (the caller has branched on fast_div), 0 the IEEE forms, -1 a branch on fast_div here
+template <int FD = -1>
 __device__ __forceinline__ float near_root(float b, float disc, const RayDiv &r, float &q)
 {
-    if (fast_div(r)) {
+    if (FD == 1 || (FD < 0 && fast_div(r))) {
         q = sqrt_scaled(disc);
         return div_ray(-b - q, r);
     }
@@ -373,11 +375,19 @@ __device__ __forceinline__ float near_root(float b, float disc, const RayDiv &r,
     return (-b - q) / r.a;
 }
 // the far root (-b + sqrt(disc)) / a, raytracer.hxx:76
+template <int FD = -1>
 __device__ __forceinline__ float far_root(float b, float q, const RayDiv &r)
 {
-    return fast_div(r) ? div_ray(-b + q, r) : (-b + q) / r.a;
+    return (FD == 1 || (FD < 0 && fast_div(r))) ? div_ray(-b + q, r) : (-b + q) / r.a;
 }
+template <int B> struct IntC { static constexpr int value = B; };
 
+#ifndef RT_GROUND1
+#define RT_GROUND1 1
+#endif
+#ifndef RT_ROOT_HOIST
+#define RT_ROOT_HOIST 5  // bit 0: blocks of 8, bit 1: of 4, bit 2: single spheres (8 and 4 together spill)
+#endif
 template <bool FAST, bool STATS, int N = 8>
 __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx, uint32_t i,
                                             f3 o, f3 d, const RayDiv &rd, Hit &h, Dbg &dbg)
@@ -426,8 +436,9 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
     // compare alone. (Formed as `pos && kt < h.key`, the mask would be ANDed into VCC by a
     // scalar op, and a VALU read of a VCC that a scalar op wrote stalls ~20 cycles on gfx950,
     // scripts/ubench_int.hip.)
-    if (ballot(mq[0] > 0.f)) {
-        if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
+    // The root form is chosen once for the block's roots (one uniform branch, not one per root)
+    auto roots = [&](auto fdc) {
+        constexpr int FD = decltype(fdc)::value;
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             const bool pos = dq[k] > 0.f;                                    // :62
@@ -436,10 +447,10 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
                 if (STATS) { dbg.lane_roots += pos; if (first_active_lane()) ++dbg.wave_roots; }
                 const float dk = pos ? dq[k] : -1.f;
                 float q;
-                float t = near_root(bq[k], dk, rd, q);                       // :63
+                float t = near_root<FD>(bq[k], dk, rd, q);                   // :63
                 const bool ok = in_range(t);
                 if (posm & ~ballot(ok)) {
-                    const float t2 = far_root(bq[k], q, rd);                 // :76
+                    const float t2 = far_root<FD>(bq[k], q, rd);             // :76
                     t = ok ? t : (in_range(t2) ? t2 : __builtin_nanf(""));
                 } else {
                     t = ok ? t : __builtin_nanf("");
@@ -448,6 +459,12 @@ __device__ __forceinline__ void test_block8(const float4 *__restrict__ geo, cons
                 if (kt < h.key) h.key = kt;
             }
         }
+    };
+    if (ballot(mq[0] > 0.f)) {
+        if (STATS) { ++dbg.lane_blocks; if (first_active_lane()) ++dbg.wave_blocks; }
+        constexpr bool hoist = (RT_ROOT_HOIST >> (N == 8 ? 0 : N == 4 ? 1 : 2)) & 1;
+        if (hoist && fast_div(rd)) roots(IntC<1>{});
+        else roots(IntC<hoist ? 0 : -1>{});
     }
 }
 
@@ -709,7 +726,10 @@ __device__ __forceinline__ Hit closest_hit(const KP &p, const float4 *__restrict
     // active: this lane traces a segment; am: the wave's mask of such lanes; key0: a candidate
     // already found for this segment (hint_candidate) or no_hit()
     Hit h{key0};
-    run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
+    // one always-tested sphere (the ground of the reference's scenes): its block without the
+    // list's loop control
+    if (RT_GROUND1 && p.n_always == 1u) test_block8<FAST, STATS, 1>(geo, sidx, 0, o, d, rd, h, dbg);
+    else run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);
     if (CULL) {
         // 1/x with its magnitude clamped to 1e30 (one med3; |x| < 1e-30 behaves as 1e-30 of
         // the same sign, zeros included): products with coordinates stay finite
@@ -768,6 +788,19 @@ __device__ __forceinline__ float4 gld4(const float4 *p, uint32_t i)
 {
     const __attribute__((address_space(1))) float *g = (const __attribute__((address_space(1))) float *)(p + i);
     return make_float4(g[0], g[1], g[2], g[3]);
+}
+// sphere ib's dielectric record {1 / ior, x(ior), x(1 / ior), shortcut word}, x(r) = (1 - r) / (1 + r),
+// from LDS or global memory (the blob's tail)
+template <int V, class KP>
+__device__ __forceinline__ float4 dielectric_record(const KP &P, const float4 *blob, uint32_t ib)
+{
+    const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
+    if (V != V_EXACT_SCALAR && P.shade_lds) {
+        const float4 r = blob[di];
+        asm volatile("");  // no merged (flat) load with the global branch
+        return r;
+    }
+    return gld4(P.blob, di);
 }
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 1  // measured: forcing 8 waves (64 VGPRs) spills and runs slower
@@ -1294,14 +1327,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                         } else {                                // dielectric, :158-194
                             RT_EV(EV_DIELECTRIC);
                             // {1 / ior, x(ior), x(1 / ior), shortcut word} of this sphere, x(r) = (1 - r) / (1 + r)
-                            const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
-                            float4 dcs;
-                            if (V != V_EXACT_SCALAR && P.shade_lds) {
-                                dcs = blob[di];
-                                asm volatile("");  // no merged (flat) load, as above
-                            } else {
-                                dcs = gld4(P.blob, di);
-                            }
+                            const float4 dcs = dielectric_record<V>(P, blob, ib);
                             {   // the next segment tests this sphere first (hint_candidate)
                                 const uint32_t sl = thread_slot(wave_base);
                                 lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);  // its geo entry, raytracer.hxx:58

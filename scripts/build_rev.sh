@@ -1,13 +1,14 @@
 #!/usr/bin/env bash
 # Build the product library of git revision <rev> into scripts/_abl/<name>/ (A/B against the
-# working tree):   scripts/build_rev.sh <name> <rev> [-DFLAG ...]
+# working tree; rev WT = the working tree itself):   scripts/build_rev.sh <name> <rev> [-DFLAG ...]
 set -eu
 name=$1; rev=$2; shift 2
 repo="$(cd "$(dirname "$0")/.." && pwd)"
 src=$(mktemp -d)
 for f in raytracinginoneweekend_amd/csrc/rt_kernel.hip raytracinginoneweekend_amd/csrc/rt_host.cpp \
          raytracinginoneweekend_amd/csrc/rt_device.h include/rt_api.h; do
-  mkdir -p "$src/$(dirname $f)"; git -C "$repo" show "$rev:$f" > "$src/$f"
+  mkdir -p "$src/$(dirname $f)"
+  if [ "$rev" = WT ]; then cp "$repo/$f" "$src/$f"; else git -C "$repo" show "$rev:$f" > "$src/$f"; fi
 done
 out=$repo/scripts/_abl/$name
 mkdir -p $out

@@ -14,18 +14,27 @@ from collections import defaultdict
 ap = argparse.ArgumentParser()
 ap.add_argument("root")
 ap.add_argument("--split-ms", type=float, default=1.8)
+ap.add_argument("--timed", action="store_true",
+                help="only the timed instantiations (render_kernel<0, 7, false, false>, render_deep_kernel<0, false, false>)")
 a = ap.parse_args()
+
+
+def wanted(name):
+    if "render_kernel" not in name and "render_deep_kernel" not in name:
+        return False
+    return not a.timed or "<0, 7, false, false>" in name or "render_deep_kernel<0, false, false>" in name
+
 groups = {"main": defaultdict(list), "deep": defaultdict(list)}
 for d in sorted(x for x in glob.glob(os.path.join(a.root, "p*")) if os.path.isdir(x)):
     dur, deep = {}, set()
     for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))):
-        if "render_kernel" in r["Kernel_Name"] or "render_deep_kernel" in r["Kernel_Name"]:
+        if wanted(r["Kernel_Name"]):
             dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
             if "render_deep_kernel" in r["Kernel_Name"]:
                 deep.add(r["Dispatch_Id"])
     per = defaultdict(float)
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if "render_kernel" in r["Kernel_Name"] or "render_deep_kernel" in r["Kernel_Name"]:
+        if wanted(r["Kernel_Name"]):
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     def kind(di):
         if deep:

@@ -105,6 +105,9 @@ def parse():
                          "de-interleave copy), to see whether that work waits for CU slots")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_render_c3.json"),
                     help="PMC summary of this kernel (scripts/pmc_round.sh) for roofline.traffic / VALU busy")
+    ap.add_argument("--options", default="",
+                    help="rt_options for the scene, rt_options_parse syntax (e.g. 'max_workspace_bytes=4294967296,"
+                         "render_streams=4'): over the library defaults and RT_OPTIONS; recorded in config.options")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher self-test (CPU): every rank joins a gloo group, prints its rank/world and "
                          "exits before any GPU call")
@@ -273,13 +276,6 @@ def pmc_fields(path, kernel, config):
     return rec, "current build of the timed kernel"
 
 
-def frames_in_flight():
-    """Render streams (RT_PIPELINE, rt_host.cpp pipeline_env: by default GPU_MAX_HW_QUEUES - 1,
-    within 2..7)."""
-    v = os.environ.get("RT_PIPELINE", "")
-    if v:
-        return max(1, min(int(v), 8))
-    return max(2, min(env_int("GPU_MAX_HW_QUEUES", 4) - 1, 7))
 
 
 def cpu_info():
@@ -346,8 +342,15 @@ def cpu_baseline(cfg, camera, seed, rows, threads):
     t0 = time.perf_counter()
     O.render_f32(s, m, cam, p, threads=threads)
     so = time.perf_counter() - t0
+    # The whole host: this job may use `threads` of the host's `aff` logical CPUs (the GPU box
+    # allots 16 per GPU and its operators ask jobs to keep their worker pools to that share), so
+    # the host-wide figure is the measured per-thread rate times every logical CPU: an upper
+    # bound (SMT siblings share a core), stated as an estimate, not a measurement.
+    whole = {"estimate": round(r["mrays_per_s"] / threads * aff, 2), "unit": "Mrays/s", "cores": aff,
+             "basis": f"measured {r['mrays_per_s'] / threads:.4f} Mrays/s per thread on {threads} threads x {aff} "
+                      "logical CPUs; linear in threads, an upper bound (SMT), not measured on all of them"}
     return dict(
-        value=round(r["mrays_per_s"], 4), unit="Mrays/s", kind="reference",
+        value=round(r["mrays_per_s"], 4), unit="Mrays/s", kind="reference", whole_host=whole,
         sample=f"{nrows} rows (every {step}th) of {W}x{H}, {spp} spp, {scene} scene, {camera} camera; "
                f"{r['seconds']:.1f} s wall; the rows' rate stands for the frame's (linear in rows)",
         single_thread={"value": round(r1["mrays_per_s"], 4), "cores": 1, "kind": "reference",
@@ -410,10 +413,14 @@ def main():
                          brute_force=args.traversal == "brute", cuda_compat=compat,
                          wavefront=args.variant == "wavefront")
     if rehearse and args.rehearse_blocks:
-        params.row_offset, params.row_stride = args.rehearse_rank * (H // rehearse), 1
+        # contiguous blocks of H // N rows, the last rank taking the remainder
+        blk = H // rehearse
+        params.row_offset, params.row_stride = args.rehearse_rank * blk, 1
+        params.num_rows = blk if args.rehearse_rank < rehearse - 1 else H - blk * (rehearse - 1)
     rows = params.num_rows
     dev = torch.device("cuda", local)
-    ds = rt.DeviceScene(arrays, device=local)
+    opts = rt.parse_options(args.options, rt.default_options())
+    ds = rt.DeviceScene(arrays, device=local, options=opts)
     tile = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
     rgb8 = args.output == "rgb8"
     tile8 = torch.empty((rows, W, 3), dtype=torch.uint8, device=dev) if rgb8 else None
@@ -527,6 +534,7 @@ def main():
     mode = rt.CORRECTED if args.camera == "corrected" else rt.REFERENCE
     cam = rt.Camera.cuda(W, H) if compat else rt.Camera.default(W, H, mode)
     main_m = summary(*measure(cam, args.steps, args.warmup, check_parity=not compat), args.steps)
+    usage = ds.usage()  # the cut of the timed frames (before the corrected-camera frames)
     corr = None
     if args.corrected_steps > 0 and not compat and args.camera == "reference":
         # the representative path-tracing load (7 segments per primary): the corrected camera
@@ -556,10 +564,10 @@ def main():
                        + ("u8 (gamma epilogue per rank)" if rgb8 else "f32") + " tiles",
                        "output": args.output, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "hw_queues_env": hw_env,
-                       # deep-path split: split depth, and the pass size below which
-                       # passes are not split (library defaults unless set in the environment)
-                       "deep_split": env_int("RT_DEEP_SPLIT", 8),
-                       "deep_min_items": env_int("RT_DEEP_MIN_ITEMS", 1 << 25)},
+                       # the scene's rt_options (library defaults, RT_OPTIONS, --options): deep-path
+                       # split and the lone-pass size below which passes are not split
+                       "deep_split": opts.deep_split, "deep_min_items": opts.deep_min_items,
+                       "options": {k: getattr(opts, k) for k, _ in rt.abi.RtOptions._fields_ if k != "size"}},
             # ms_per_step is the steady-state period of a frame stream (frames in flight);
             # frame_wall_ms is ONE frame alone, start to finish, ending with the frame in host
             # memory as the reference's entry returns it (render, accumulate, gather, D2H copy
@@ -568,7 +576,13 @@ def main():
             "frame_wall_ms": r3(main_m["frame_wall_ms"]),
             "frame_device_ms": r3(main_m["frame_latency_ms"]),
             "frame_latency_ms": r3(main_m["frame_latency_ms"]),
-            "frames_in_flight": frames_in_flight(),
+            # render streams the timed frames rotated over (frames in flight), the workspaces and
+            # the samples per pass (rt_scene_usage_get after the run)
+            "frames_in_flight": usage["render_streams"], "workspaces": usage["workspaces"],
+            "pass_samples": usage["pass_samples"],
+            # device memory the scene held for the timed frames: HBM footprint of the product
+            # (scene blobs, counters, slot workspaces, deep-path queues), and the workspaces alone
+            "hbm_footprint_bytes": usage["device_bytes"], "hbm_workspace_bytes": usage["workspace_bytes"],
             "segments_per_primary": round(main_m["segments_per_primary"], 4),
             "msegments_per_s": round(main_m["msegments_per_s"], 1),
             "gtests_per_s": round(main_m["gtests_per_s"], 2),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 1
+#define RT_API_VERSION 2  /* 2: rt_options (resource bounds and A/B toggles), rt_scene_usage */
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum rt_status {
@@ -101,8 +101,8 @@ enum rt_flags {
                                        CPU path: src/CUDA/cuda_impl.cu (see rt_render_cuda_impl) */
     RT_FLAG_WAVEFRONT = 1u << 5     /* A/B: the wavefront variant (one launch per segment, ray
                                        queues in HBM) instead of the persistent megakernel;
-                                       same bits, cluster culling; RT_WAVE_QUEUE_RAYS bounds a
-                                       chunk (default 2^25 rays, 52 B each, two queues)          */
+                                       same bits, cluster culling; rt_options.wave_queue_rays
+                                       bounds a chunk (2^25 rays, 52 B each, two queues)       */
 };
 typedef struct rt_params {
     uint32_t width, height;
@@ -125,6 +125,64 @@ typedef struct rt_stats {
 int rt_version(void);
 const char *rt_last_error(void);
 int rt_device_count(int *count);
+
+/* ---- options: resource bounds and same-bits variants of a scene ---------------------
+ * rt_options_default() fills the library defaults; change fields, then pass the record to
+ * rt_scene_create_ex / rt_multi_create_ex, or make it the process default
+ * (rt_set_default_options) for scenes created without one: rt_scene_create, the synchronous
+ * renders (rt_render_f32, rt_render_rgb8, rt_render_multi_*) and rt_multi_create.
+ * The environment variable RT_OPTIONS ("key=value,key=value", keys as the field names, the
+ * diag bits as ieee_roots=1 ...; rt_options_parse) is applied over the defaults once, at the
+ * library's first use, so an unmodified caller (the reference's main() with the drop-in) can
+ * be A/B-tested. Every value is checked: RT_ERR_INVALID names the field. No option changes
+ * a rendered bit (every variant is the reference's arithmetic); they trade memory and speed. */
+typedef struct rt_options {
+    uint32_t size;                  /* sizeof(rt_options): the record's revision              */
+    uint32_t render_streams;        /* frames in flight: internal render streams. 0 = auto
+                                       (GPU_MAX_HW_QUEUES - 1, within 2..7), 1 = every kernel
+                                       on the caller's stream, 2..8                           */
+    uint32_t workspaces_per_stream; /* sample-slot workspaces per render stream, 1..2 (2)     */
+    uint32_t deep_split;            /* paths past this many segments finish in a second, dense
+                                       launch; 0 = no split, 1..1024 (8)      */
+    uint64_t max_pass_bytes;        /* slot workspace of one pass (12 B per pixel and sample):
+                                       12 B .. 2 GiB (2 GiB); frames above it run in passes    */
+    uint64_t max_workspace_bytes;   /* cap on the scene's device workspaces (slots, deep-path
+                                       queues, multi-pass sums, wavefront queues); 0 = none.
+                                       Over it, passes shrink (to 4 samples), then workspaces
+                                       per stream, then streams go; RT_ERR_CAPACITY if one
+                                       4-sample pass on the caller's stream does not fit       */
+    uint64_t deep_min_items;        /* a pass issued while no other render runs (a lone frame)
+                                       is split only from this many samples (2^25); passes
+                                       issued beside other renders are split at any size       */
+    uint32_t cluster_size;          /* spheres per culling cluster, 4..64, a multiple of 4 (16);
+                                       read when the scene is created                         */
+    uint32_t transpose_max;         /* clusters requested by at most this many lanes run as
+                                       (ray, member) pairs over the wave, 0..16 (16)           */
+    uint32_t wave_queue_rays;       /* RT_FLAG_WAVEFRONT: rays per chunk, >= 64 (2^25)        */
+    uint32_t diag;                  /* rt_diag bits (0)                                        */
+} rt_options;
+enum rt_diag {
+    RT_DIAG_IEEE_ROOTS = 1u << 0,      /* the IEEE sqrt/division sequences for every root     */
+    RT_DIAG_NO_SHORTCUT = 1u << 1,     /* no walk shortcut for rays in glass balls            */
+    RT_DIAG_NO_NEIGHBOURS = 1u << 2,   /* the shortcut for isolated balls only                */
+    RT_DIAG_NO_ROOT_BOX = 1u << 3,     /* no level-3 box gate before the cluster walk         */
+    RT_DIAG_SHADE_LDS = 1u << 4,       /* shading records forced into LDS ...                 */
+    RT_DIAG_SHADE_GLOBAL = 1u << 5,    /* ... or into global memory (default: by occupancy)   */
+    RT_DIAG_STATS = 1u << 6,           /* the instrumented kernel (rt_scene_debug_*)           */
+    RT_DIAG_STATS_DEEP_ONLY = 1u << 7, /* with STATS: count the deep launch alone             */
+    RT_DIAG_VERBOSE = 1u << 8,         /* print every launch's plan to stderr                 */
+    RT_DIAG_STANDIN_TRANSPORT = 1u << 9 /* rt_multi with every rank on one device: the RCCL
+                                          gather code path, RCCL replaced by stream-ordered
+                                          device copies (tests of that path on one GPU)       */
+};
+int rt_options_default(rt_options *out);
+/* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,
+ * no_neighbours, no_root_box, shade_lds, shade_global, stats, stats_deep_only, verbose,
+ * standin_transport = 0/1) to *inout; RT_ERR_INVALID on an unknown key or a bad value.   */
+int rt_options_parse(const char *text, rt_options *inout);
+/* The options of scenes created without explicit ones (NULL: the library defaults).      */
+int rt_set_default_options(const rt_options *options);
+int rt_get_default_options(rt_options *out);
 
 /* ---- host-side scene / camera construction ----------------------------------------- */
 /* raytracer::camera ctor, src/camera.hxx:24-44 (aperture -> lens_radius = aperture/2). */
@@ -196,19 +254,35 @@ typedef struct rt_scene rt_scene;
 int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres,
                     const rt_material *materials, uint32_t n_materials, int device,
                     rt_scene **out);
+/* The same with explicit options (NULL: the process default, rt_set_default_options).   */
+int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres,
+                       const rt_material *materials, uint32_t n_materials, int device,
+                       const rt_options *options, rt_scene **out);
 int rt_scene_destroy(rt_scene *scene);
 /* Enqueue one render for `stream` (a hipStream_t, or NULL for the null stream).
  * d_rgb: device buffer laid out as rt_params says. d_segments: optional device u64[3]
  * that accumulates {segments, sphere tests, cluster box tests} (zero it first). No
- * host sync (a call whose slot workspace or accumulation buffer must grow synchronises the
- * device once, before enqueuing). The render kernels rotate over the scene's internal streams (the process's
- * hardware queues - 1: 3 at HIP's default GPU_MAX_HW_QUEUES=4, at most 4) and 2 slot
- * workspaces per stream, so consecutive frames overlap; they read only the scene and the by-value
- * arguments, and the writes to d_rgb / d_segments are enqueued on `stream`, so results appear
- * in stream order (RT_PIPELINE=n in the environment sets the streams, 2..8; 0: all on
- * `stream`).                                                                                 */
+ * host sync (a call whose workspaces must grow, or be re-cut under max_workspace_bytes,
+ * synchronises the device once, before enqueuing). The render kernels rotate over the
+ * scene's internal render streams (rt_options.render_streams: by default the process's
+ * hardware queues - 1, i.e. 3 at HIP's default GPU_MAX_HW_QUEUES=4 and at most 7) with
+ * rt_options.workspaces_per_stream slot workspaces each, so consecutive frames overlap; they
+ * read only the scene and the by-value arguments, and the writes to d_rgb / d_segments are
+ * enqueued on `stream`, so results appear in stream order.                                   */
 int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *params,
                      float *d_rgb, void *stream, uint64_t *d_segments);
+/* Device memory a scene holds and how its renders are cut (after the last render call).  */
+typedef struct rt_scene_usage {
+    uint64_t device_bytes;     /* every device allocation of the scene                       */
+    uint64_t workspace_bytes;  /* of which workspaces (bounded by max_workspace_bytes)       */
+    uint32_t render_streams;   /* streams the last render rotated over (1: caller's only)    */
+    uint32_t workspaces;       /* slot workspaces in use                                     */
+    uint32_t pass_samples;     /* samples per pass of the last render                        */
+    uint32_t static_lds_bytes; /* the culled render kernel's static LDS per workgroup        */
+    uint32_t max_lds_bytes;    /* the device's LDS per workgroup                              */
+    uint32_t reserved;
+} rt_scene_usage;
+int rt_scene_usage_get(const rt_scene *scene, rt_scene_usage *out);
 /* Spans (ms, HIP events) of the render kernels of the most recent calls of
  * rt_render_device on this scene, oldest first: entry i runs from the start event of the
  * call's first pass to the end event of its last pass. Consecutive calls' launches run
@@ -216,7 +290,7 @@ int rt_render_device(rt_scene *scene, const rt_camera *camera, const rt_params *
  * calls' renders and accumulations: it is a latency, not a per-frame cost. Writes up to
  * `max` entries, *n = entries written. Waits for those calls to finish.                 */
 int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n);
-/* Diagnostics: with RT_DEBUG_STATS=1 in the environment, renders on this scene use an
+/* Diagnostics: with RT_DIAG_STATS in the scene's options, its renders use an
  * instrumented kernel (identical output) that tallies: [0] wave loop iterations,
  * [1] wave refill rounds, [2] wave / [3] lane sphere blocks with a positive discriminant,
  * [4] wave / [5] lane root evaluations, [6] segments, [7] wave-level blocks of 8 cluster
@@ -227,9 +301,9 @@ int rt_scene_debug_counters(rt_scene *scene, uint64_t out[16], int reset);
 /* Diagnostics: per-wave records of the last instrumented render launch, out[4w .. 4w+3] for
  * wave w of the grid = {time the wave found every queue dry, exit} (100 MHz realtime
  * clock), loop iterations, and (hardware CU id << 32 | iterations after dry << 16 | refill
- * rounds); at most max_waves records, *n = records written (0 without RT_DEBUG_STATS=1).  */
+ * rounds); at most max_waves records, *n = records written (0 without RT_DIAG_STATS).      */
 int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, uint32_t *n);
-/* Diagnostics: with RT_DEBUG_STATS=1, how often each block of the render loop ran, counted once
+/* Diagnostics: with RT_DIAG_STATS, how often each block of the render loop ran, counted once
  * per wave per execution, summed over the instrumented launches since the last reset: [0] loop
  * iterations, [1] refill trips, [2] sample starts, [3] rejection attempts, [4] lens rays done,
  * [5] scatters done, [6] root-box passes, [7] level-2 boxes walked, [8] level-2 boxes passed,
@@ -255,6 +329,11 @@ enum rt_output_format { RT_OUTPUT_F32 = 0, RT_OUTPUT_RGB8 = 1 };
 int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres,
                     const rt_material *materials, uint32_t n_materials,
                     const int *devices, int n_ranks, rt_multi **out);
+/* The same with explicit options for every rank's scene (NULL: the process default).     */
+int rt_multi_create_ex(const rt_sphere *spheres, uint32_t n_spheres,
+                       const rt_material *materials, uint32_t n_materials,
+                       const int *devices, int n_ranks, const rt_options *options,
+                       rt_multi **out);
 int rt_multi_destroy(rt_multi *ctx);
 /* n_ranks, and whether the gather runs over RCCL (1) or device copies (0).              */
 int rt_multi_info(const rt_multi *ctx, int *n_ranks, int *uses_rccl);

@@ -239,9 +239,10 @@ raytracer::camera make_camera(const args_t &a)
         0.0625f, math::distance(math::vec3{-4, 3.2, 5}, math::vec3{0, 1, 0})};
 }
 
-// Renders rows y = row0 + i*row_step, i < nrows, of the W x H frame, one thread per
-// interleaved subset of those rows (PCG build only; the verbatim mt19937 build shares
-// one stream across the frame and must run on one thread, as the reference does).
+// Renders rows y = row0 + i*row_step, i < nrows, of the W x H frame; threads take runs of 64
+// pixels of those rows from a shared counter (dynamic, so that 256 threads stay busy on a
+// frame of 720 rows of uneven cost; PCG build only: the verbatim mt19937 build shares one
+// stream across the frame and must run on one thread, as the reference does).
 void render(const args_t &a, const std::vector<sphere_rec> &S, const std::vector<material_rec> &M,
             std::vector<float> &f32, std::vector<std::uint8_t> &u8)
 {
@@ -252,6 +253,7 @@ void render(const args_t &a, const std::vector<sphere_rec> &S, const std::vector
 #ifndef RT_REF_ENGINE_PCG
     T = 1;
 #endif
+    std::atomic<std::uint64_t> next_run{0};
     auto worker = [&](unsigned tid) {
         raytracer::data raytracer_data;
         records_to_scene(S, M, raytracer_data);
@@ -262,10 +264,16 @@ void render(const args_t &a, const std::vector<sphere_rec> &S, const std::vector
 #endif
         std::vector<math::vec3> multisampling_texels(a.spp, math::vec3{0});
         auto random_distribution = std::uniform_real_distribution{0.f, 1.f};
-        for (std::uint32_t i = tid; i < nrows; i += T) {
+        (void)tid;
+        const std::uint32_t runs_per_row = (a.W + 63u) / 64u;
+        for (;;) {
+            const std::uint64_t run = next_run.fetch_add(1, std::memory_order_relaxed);
+            if (run >= (std::uint64_t)nrows * runs_per_row) break;
+            const std::uint32_t i = static_cast<std::uint32_t>(run / runs_per_row);
+            const std::uint32_t x0 = static_cast<std::uint32_t>(run % runs_per_row) * 64u;
             const std::uint32_t y = a.row0 + i * a.row_step;
             auto v = static_cast<float>(y) / static_cast<float>(a.H);
-            for (auto x = 0u; x < a.W; ++x) {
+            for (auto x = x0; x < std::min(a.W, x0 + 64u); ++x) {
                 auto u = static_cast<float>(x) / static_cast<float>(a.W);
                 std::uint32_t s = 0;
                 std::generate(std::execution::par, std::begin(multisampling_texels), std::end(multisampling_texels), [&]() {

@@ -57,6 +57,31 @@ class RtParams(C.Structure):
     ]
 
 
+class RtOptions(C.Structure):
+    """rt_options (include/rt_api.h): resource bounds and same-bits variants of a scene."""
+    _fields_ = [
+        ("size", C.c_uint32), ("render_streams", C.c_uint32), ("workspaces_per_stream", C.c_uint32),
+        ("deep_split", C.c_uint32), ("max_pass_bytes", C.c_uint64), ("max_workspace_bytes", C.c_uint64),
+        ("deep_min_items", C.c_uint64), ("cluster_size", C.c_uint32), ("transpose_max", C.c_uint32),
+        ("wave_queue_rays", C.c_uint32), ("diag", C.c_uint32),
+    ]
+
+
+class RtSceneUsage(C.Structure):
+    _fields_ = [
+        ("device_bytes", C.c_uint64), ("workspace_bytes", C.c_uint64), ("render_streams", C.c_uint32),
+        ("workspaces", C.c_uint32), ("pass_samples", C.c_uint32), ("static_lds_bytes", C.c_uint32),
+        ("max_lds_bytes", C.c_uint32), ("reserved", C.c_uint32),
+    ]
+
+
+RT_DIAG = {
+    "ieee_roots": 1 << 0, "no_shortcut": 1 << 1, "no_neighbours": 1 << 2, "no_root_box": 1 << 3,
+    "shade_lds": 1 << 4, "shade_global": 1 << 5, "stats": 1 << 6, "stats_deep_only": 1 << 7, "verbose": 1 << 8,
+    "standin_transport": 1 << 9,
+}
+
+
 class RtStats(C.Structure):
     _fields_ = [
         ("primaries", C.c_uint64), ("segments", C.c_uint64), ("sphere_tests", C.c_uint64),
@@ -70,6 +95,7 @@ MATERIAL_DTYPE = np.dtype([("kind", "<u4"), ("albedo", "<f4", (3,)), ("param", "
 assert SPHERE_DTYPE.itemsize == C.sizeof(RtSphere) == 20
 assert MATERIAL_DTYPE.itemsize == C.sizeof(RtMaterial) == 20
 assert C.sizeof(RtParams) == 40
+assert C.sizeof(RtOptions) == 56 and C.sizeof(RtSceneUsage) == 40
 
 
 def ptr(arr, ctype=C.c_void_p):

@@ -72,6 +72,15 @@ def _declare(L):
         "rt_scene_debug_timeline": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint32, P(C.c_uint32)]),
         "rt_scene_debug_events": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int]),
         "rt_epilogue_rgb8_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+        "rt_options_default": (C.c_int, [P(abi.RtOptions)]),
+        "rt_options_parse": (C.c_int, [C.c_char_p, P(abi.RtOptions)]),
+        "rt_set_default_options": (C.c_int, [P(abi.RtOptions)]),
+        "rt_get_default_options": (C.c_int, [P(abi.RtOptions)]),
+        "rt_scene_create_ex": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32, C.c_int,
+                                         P(abi.RtOptions), P(C.c_void_p)]),
+        "rt_scene_usage_get": (C.c_int, [C.c_void_p, P(abi.RtSceneUsage)]),
+        "rt_multi_create_ex": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32, P(C.c_int),
+                                         C.c_int, P(abi.RtOptions), P(C.c_void_p)]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("RT_LIB_PATH") and not hasattr(L, name):

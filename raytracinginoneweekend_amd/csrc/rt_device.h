@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rt_consts.h"
+
 namespace rt {
 
 // Work decomposition:
@@ -18,18 +20,10 @@ namespace rt {
 //     (a multi-sample item on a deep path holds its wave long after the queues are dry).
 //   items of one launch (a "pass"): samples [sample_begin, sample_end) x all pixels, item I ->
 //     sample sample_begin + I / n_pixels, pixel I % n_pixels; passes start on multiples of 4.
-//     Chunks of chunk_items consecutive items are dealt from 8 queues (chunk c belongs to
-//     queue c % 8) by per-queue atomic counters.
+//     Blocks of 64 consecutive items are dealt from 8 queues (queue q owns the q-th eighth of
+//     the blocks) in guided chunks, one per-queue atomic ticket each.
 // Per-render constants used only where a sample or an item starts (the kernel re-reads them
 // from the kernarg segment at each use; see render_kernel).
-// Exact unsigned division by a per-render invariant d (Granlund-Montgomery, "round-up with
-// add"): q = (t + ((n - t) >> s1)) >> s2, t = mulhi(n, m), for every 32-bit n; d >= 2: s1 = 1,
-// s2 = ceil(log2 d) - 1, m = floor(2^32 (2^ceil(log2 d) - d) / d) + 1; d = 1: m = s1 = s2 = 0
-// (t = 0, q = n), so no branch.
-struct UDiv {
-    uint32_t m, s1, s2;
-};
-
 struct FrameConsts {
     float org[3], llc[3], hor[3], ver[3];
     float lens, fW, fH;
@@ -74,10 +68,9 @@ struct KParams {
     uint32_t n_pixels, tiles_x, tiled_rows;  // tiled_rows: rows covered by 64-pixel tiles (0 = untiled)
     uint32_t tile_lw;                       // log2 of the tile width (3: 8x8, 4: 16x4, 5: 32x2, 6: 64x1)
     uint32_t sample_begin, sample_end;      // this launch's samples
-    uint32_t n_items, n_chunks, chunk_items;  // items dealt per queue grab (multiple of 64)
-    uint32_t n_big_chunks;   // chunks [0, n_big_chunks) hold chunk_items items, the rest 64
+    uint32_t n_items;
     uint32_t n_blocks;       // guided dealing: ceil(n_items / 64) blocks, 1/8 per queue
-    float guided_l2b;        // log2(beta) < 0: guided dealing (rt_kernel.hip refill); 0: fixed chunks
+    float guided_l2b;        // log2(beta) < 0 of the guided dealing (rt_kernel.hip refill)
     // scene
     uint32_t n_spheres, n_materials;
     // scene blob, staged whole into LDS: [geo: n_geo float4 {cx, cy, cz, fl(r*r)}]
@@ -171,13 +164,6 @@ struct KWave {
     uint32_t cap;            // queue capacity (rays)
     uint32_t item_begin, n_chunk;  // wave_gen_kernel: items [item_begin, item_begin + n_chunk)
 };
-
-// A lane inside an isolated dielectric sphere (rt_host.cpp isolated_spheres) skips the cluster
-// walk when both ends of its segment lie within the ball |p - C|^2 <= fl(fl(r r) kIsoR2Grow)
-constexpr float kIsoR2Grow = 1.0201f;
-// a dielectric sphere's shortcut word (rt_host.cpp shortcut_words): this bit, then the geo slots
-// (+ 1, 0 = none) of its at most two neighbours in bits [0, 15) and [15, 30)
-constexpr uint32_t kShortcut = 0x80000000u;
 
 // queue counters sit on separate 256-byte lines so the 8 queues' atomics do not serialise
 constexpr uint32_t kQueueStride = 64;

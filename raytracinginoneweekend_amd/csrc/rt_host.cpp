@@ -1,14 +1,14 @@
-// rt_host.cpp — host side of the C-ABI (include/rt_api.h): scene/camera construction that
-// mirrors the reference's host code bit for bit, device scene upload, pass planning and the
-// render entry points that replace `cuda_impl` (src/main.cxx:18, src/CUDA/cuda_impl.cu:384).
-//
-// Compiled with -ffp-contract=off: the camera basis and the huge-scene generator must round
-// exactly like the reference's (g++, x86-64 SSE, no contraction).
+// rt_host.cpp — the device half of the C-ABI's host side (include/rt_api.h): device scene upload,
+// pass planning under the scene's options, frames in flight, the render entry points that replace
+// `cuda_impl` (src/main.cxx:18, src/CUDA/cuda_impl.cu:384) and the multi-GPU context. The
+// host-only half (camera and scene constructors, cluster builder, options, PPM writer) is
+// rt_host_build.cpp.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -24,10 +24,14 @@
 
 #include "../../include/rt_api.h"
 #include "rt_device.h"
+#include "rt_host_build.h"
+
+using namespace rthost;
 
 namespace rt {
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream);
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
+hipError_t static_lds_render(int variant, int cull, size_t *bytes);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream);
 hipError_t launch_wave_gen(const KWave &w, hipStream_t stream);
@@ -39,13 +43,6 @@ hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_
 
 namespace {
 
-thread_local std::string g_error;
-
-int fail(int code, const std::string &msg)
-{
-    g_error = msg;
-    return code;
-}
 
 #define RT_HIP(call)                                                                      \
     do {                                                                                  \
@@ -54,91 +51,28 @@ int fail(int code, const std::string &msg)
             return fail(RT_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-// ---- host vector math in the reference's evaluation order (src/math.hxx) ------------
-struct hv { float x, y, z; };
-hv operator+(hv a, hv b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-hv operator-(hv a, hv b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-hv operator*(hv a, float s) { return {a.x * s, a.y * s, a.z * s}; }
-float hlen(hv a) { return std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
-hv hnorm(hv a)
-{
-    float l = hlen(a);
-    return std::fabs(l) > FLT_MIN ? hv{a.x / l, a.y / l, a.z / l} : a;
-}
-hv hcross(hv l, hv r) { return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x}; }
 
-constexpr uint64_t kMaxSlotsBytes = 1ull << 31;  // slot workspace per pass (2 GiB)
-// (the kernel forms a slot index sample * n_pixels + pixel in 32 bits)
-static_assert(kMaxSlotsBytes / 12 < (1ull << 32), "slot index width");
-// 2 x 8 queue lines, 2 x 4 u64 segment counters, then the compat kernel's pixel counter
-// internal render streams for frames in flight (RT_PIPELINE = 2..kMaxBufs), and workspaces:
-// RT_WS_PER_STREAM (1..2) per stream, at most kMaxWs
-constexpr uint32_t kMaxBufs = 8;
-constexpr uint32_t kMaxWs = 2 * kMaxBufs;
-constexpr uint32_t kDeepSplitDefault = 8;  // RT_DEEP_SPLIT
 // counters: [kMaxWs][8 queues x kQueueStride], then [kMaxWs][4] u64 segment counters, then
 // the compat kernel's counter
 constexpr size_t kSegWords = kMaxWs * 8 * rt::kQueueStride;
 constexpr size_t kCompatCtr = kSegWords + kMaxWs * 8 + 16;
 constexpr size_t kCtrWords = kCompatCtr + rt::kQueueStride;
 
-// RT_WAVE_QUEUE_RAYS: rays per chunk of the wavefront variant (default 2^25: 2 x 1.7 GB queues)
-uint64_t wave_queue_env()
-{
-    const char *e = std::getenv("RT_WAVE_QUEUE_RAYS");
-    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
-    return v ? std::max<uint64_t>(v, 64) : (1ull << 25);
-}
 
-// RT_SLOT_BUDGET_BYTES lowers the per-pass slot workspace (tests force multi-pass renders).
-uint64_t slot_budget()
-{
-    const char *e = std::getenv("RT_SLOT_BUDGET_BYTES");
-    const unsigned long long v = e ? std::strtoull(e, nullptr, 10) : 0ull;
-    return v ? std::min<uint64_t>(v, kMaxSlotsBytes) : kMaxSlotsBytes;
-}
-
-// Items per queue grab (RT_CHUNK_ITEMS for A/B: a multiple of 64 in [64, 8192]); bigger
-// chunks mean fewer cross-XCD atomics, smaller ones a finer end-of-launch balance.
-uint32_t chunk_items()
-{
-    const char *e = std::getenv("RT_CHUNK_ITEMS");
-    const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 0ul;
-    return v >= 64 && v <= 8192 && v % 64 == 0 ? static_cast<uint32_t>(v) : 512u;
-}
-
-// Item dealing (default guided, K = RT_GUIDED_K, default 6): each queue's chunks shrink
-// geometrically from 1/K of its remaining share per wave down to 128 items — few queue
-// atomics, big coherent chunks for most of the launch, small ones at its end. Config 3 frame
-// stream: K = 6 3.93 ms/frame with single-frame latency unchanged (5.3-5.4 ms); K = 4
-// 3.89-3.92 but 6.2 ms latency; the fixed scheme (RT_SCHED=fixed: RT_CHUNK_ITEMS chunks, the
-// last RT_TAIL_PCT % in 64s) 4.39 ms at 512/8%, 3.96 at 2048/2% (5.7 ms latency).
-// Round 3: a pass issued while no other render runs (a lone frame) deals with K = 12 — its end
-// is not hidden by other launches, and smaller last chunks even it out (config 3 lone frame
-// 3.37-3.45 vs 3.55-3.59 ms, frame stream alike at K = 6/9/12; profiles/r03/ab/guided_k.txt).
+// Item dealing (guided): each queue's chunks shrink geometrically from 1/K of its remaining
+// share per wave down to 128 items — few queue atomics, big coherent chunks for most of the
+// launch, small ones at its end. Config 3 frame stream: K = 6 3.93 ms/frame with single-frame
+// latency unchanged (5.3-5.4 ms); K = 4 3.89-3.92 but 6.2 ms latency; fixed 512-item chunks
+// with a 64-item tail 4.39 ms (round 1; the fixed scheme was removed in round 4). A pass
+// issued while no other render runs (a lone frame) deals with K = 12 — its end is not hidden
+// by other launches, and smaller last chunks even it out (config 3 lone frame 3.37-3.45 vs
+// 3.55-3.59 ms, frame stream alike at K = 6/9/12/16; profiles/r03/ab/guided_k.txt).
 float guided_l2b(uint32_t total_waves, bool in_flight)
 {
-    const char *e = std::getenv("RT_SCHED");
-    if (e && std::strcmp(e, "fixed") == 0) return 0.f;
-    const char *ke = std::getenv("RT_GUIDED_K");
-    const double k = ke && *ke ? std::max(0.25, std::atof(ke)) : (in_flight ? 6.0 : 12.0);
+    const double k = in_flight ? 6.0 : 12.0;
     const double wq = std::max(1.0, total_waves / 8.0);
     const double beta = std::max(1.0 - 1.0 / (k * wq), 1.0 / (1 << 20));
     return static_cast<float>(std::log2(beta));
-}
-
-// log2 of the tile width (RT_TILE_LW=3..6 for A/B; default 3 = 8x8 tiles). Tiles whose image
-// footprint stays near square for strided rows (16x4 at stride 2-4, 32x2 at 5-8) were not
-// faster: row shares of config 3 at N = 8: 8x8 0.61-0.62 ms, 32x2 0.62, 64x1 0.66; N = 4:
-// 8x8 1.08-1.10, 16x4 1.10, 32x2 1.14; N = 2: 8x8 1.99, 16x4 2.02-2.05.
-uint32_t tile_lw_for(uint32_t width, uint32_t stride)
-{
-    (void)stride;
-    const char *e = std::getenv("RT_TILE_LW");
-    uint32_t lw = 3u;
-    if (e && *e) lw = static_cast<uint32_t>(std::clamp<long>(std::strtol(e, nullptr, 10), 3, 6));
-    while (lw > 3 && width % (1u << lw)) --lw;  // the tile width must divide the row
-    return lw;
 }
 
 // Workgroups per CU of a render launch. A launch that finds no other render in flight (a
@@ -153,31 +87,22 @@ uint32_t tile_lw_for(uint32_t width, uint32_t stride)
 // With 4 streams (GPU_MAX_HW_QUEUES=8): grid 2: config 3 3.83-3.84 ms, 8-way 0.60-0.61; grid
 // 3: 3.84-3.86, 0.65 — but config 3 with the corrected camera (7 segments per primary, 29 ms
 // frames) 32.0-34.3 ms at grid 2 vs 29.8 at grid 3 (28.8 with 2 streams and full grids), so
-// the third applies to short passes only. RT_GRID_WG_PER_CU=n sets the in-flight grid (A/B).
+// the third applies to short passes only. Round 3 re-swept 3/5/7 (7 streams): the default best
+// or within noise (profiles/r03/ab/knobs_s3.txt).
 constexpr uint64_t kShortPassItems = 32ull << 20;
 int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams, uint64_t pass_items)
 {
     if (!in_flight) return occ;
-    const char *e = std::getenv("RT_GRID_WG_PER_CU");
-    const long v = e && *e ? std::strtol(e, nullptr, 10) : 0;
-    if (v > 0) return std::min<int>(occ, static_cast<int>(v));
     const int others = pass_items <= kShortPassItems ? std::max(1, static_cast<int>(streams) - 1)
                                                      : std::min(2, std::max(1, static_cast<int>(streams) - 1));
     return std::max(1, (occ + others - 1) / others);
-}
-
-// Share of a launch's items dealt in 64-item chunks at its end (RT_TAIL_PCT for A/B, 0-100).
-uint32_t tail_pct()
-{
-    const char *e = std::getenv("RT_TAIL_PCT");
-    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 8ul;
-    return v <= 100 ? static_cast<uint32_t>(v) : 8u;
 }
 
 } // namespace
 
 struct rt_scene {
     int device = 0;
+    rt_options opt{};  // fixed at creation (rt_scene_create_ex)
     uint32_t n_spheres = 0, n_materials = 0;
     // scene blobs: [0] every sphere in index order (brute force), [1] big
     // spheres always tested + spatial clusters
@@ -223,15 +148,18 @@ struct rt_scene {
     int last_ws = -1;       // workspace of the last render pass issued (its ev_done), -1 = none
     // the caller stream of the previous call and an event after the last work enqueued on it:
     // a call on another stream first waits for it, so the shared accumulation buffer, the
-    // compat counter and (RT_PIPELINE=0) the workspaces are never used by two streams at once
+    // compat counter and (render_streams = 1) the workspaces are never used by two streams at once
     hipStream_t last_stream = nullptr;
     hipEvent_t ev_tail = nullptr;
     bool tail_valid = false;
     int cu_count = 0;
     int occ[4][2][2];  // [variant][culled][shade records in LDS] blocks per CU, -1 = unknown
-    unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DEBUG_STATS=1)
+    unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DIAG_STATS)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
+    size_t static_lds = 0;  // the culled render kernel's static LDS (hipFuncGetAttributes)
+    // the last render's cut (rt_scene_usage_get)
+    uint32_t used_streams = 0, used_ws = 0, used_pass = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
     static constexpr uint32_t kRing = 256;
     std::vector<hipEvent_t> ev_begin, ev_end;
@@ -240,9 +168,6 @@ struct rt_scene {
 
 extern "C" {
 
-int rt_version(void) { return RT_API_VERSION; }
-
-const char *rt_last_error(void) { return g_error.c_str(); }
 
 int rt_device_count(int *count)
 {
@@ -254,412 +179,13 @@ int rt_device_count(int *count)
     return RT_OK;
 }
 
-// raytracer::camera ctor, src/camera.hxx:24-44.
-int rt_camera_init(const float position[3], const float lookat[3], const float up[3], float aspect,
-                   float vfov_degrees, float aperture, float focus_distance, uint32_t mode, rt_camera *out)
-{
-    if (!position || !lookat || !up || !out) return fail(RT_ERR_INVALID, "rt_camera_init: null argument");
-    if (mode > RT_CAMERA_CORRECTED) return fail(RT_ERR_INVALID, "rt_camera_init: bad mode");
-    const hv P{position[0], position[1], position[2]}, L{lookat[0], lookat[1], lookat[2]}, U{up[0], up[1], up[2]};
-    const float theta = (vfov_degrees * static_cast<float>(0.01745329251994329576923690768489)) / 2.f; // math.hxx:8-13
-    const float height = std::tan(theta);
-    const float width = height * aspect;
-    const hv w = hnorm(P - L);
-    const hv u = hnorm(hcross(U, w));
-    const hv v = hnorm(hcross(w, u));
-    const hv llc = P - ((u * width + v * height) + w) * focus_distance;
-    const hv hor = ((u * width) * focus_distance) * 2.f;
-    const hv ver = ((v * height) * focus_distance) * 2.f;
-    rt_camera c{};
-    c.origin[0] = P.x; c.origin[1] = P.y; c.origin[2] = P.z;
-    c.lower_left_corner[0] = llc.x; c.lower_left_corner[1] = llc.y; c.lower_left_corner[2] = llc.z;
-    c.horizontal[0] = hor.x; c.horizontal[1] = hor.y; c.horizontal[2] = hor.z;
-    c.vertical[0] = ver.x; c.vertical[1] = ver.y; c.vertical[2] = ver.z;
-    c.lens_radius = aperture / 2.f;
-    c.mode = mode;
-    *out = c;
-    return RT_OK;
-}
 
-// src/main.cxx:179-183
-int rt_camera_cuda(uint32_t width, uint32_t height, rt_camera *out)
-{
-    // cuda_impl.cu:371-375: position 0, look (0, 0, -1), up y, vFOV 88, aperture .0625, focus 1;
-    // camera::ray has no lens offset under CUDA_IMPL (camera.hxx:48-50), and with the origin at
-    // 0 the missing "- origin" does not matter
-    if (!width || !height) return fail(RT_ERR_INVALID, "rt_camera_cuda: zero size");
-    const float pos[3] = {0.f, 0.f, 0.f}, look[3] = {0.f, 0.f, -1.f}, up[3] = {0.f, 1.f, 0.f};
-    return rt_camera_init(pos, look, up, static_cast<float>(width) / static_cast<float>(height), 88.f, .0625f, 1.f,
-                          RT_CAMERA_REFERENCE, out);
-}
-
-int rt_camera_default(uint32_t width, uint32_t height, uint32_t mode, rt_camera *out)
-{
-    if (!width || !height) return fail(RT_ERR_INVALID, "rt_camera_default: zero size");
-    const float pos[3] = {-4.f, 3.2f, 5.f}, look[3] = {0.f, 1.f, 0.f}, up[3] = {0.f, 1.f, 0.f};
-    const float focus = hlen(hv{pos[0], pos[1], pos[2]} - hv{look[0], look[1], look[2]});
-    return rt_camera_init(pos, look, up, static_cast<float>(width) / static_cast<float>(height), 42.f, 0.0625f,
-                          focus, mode, out);
-}
 
 } // extern "C"
 
 namespace {
 
-struct scene_builder {
-    std::vector<rt_sphere> s;
-    std::vector<rt_material> m;
-    void mat(uint32_t kind, float r, float g, float b, float param) { m.push_back({kind, {r, g, b}, param}); }
-    void sph(float x, float y, float z, float radius, uint32_t mi) { s.push_back({{x, y, z}, radius, mi}); }
-    void simple()  // src/main.cxx:120-129
-    {
-        mat(RT_LAMBERT, static_cast<float>(.1), static_cast<float>(.2), static_cast<float>(.5), 0.f);
-        mat(RT_METAL, static_cast<float>(.8), static_cast<float>(.6), static_cast<float>(.2), 0.f);
-        mat(RT_DIELECTRIC, 1.f, 1.f, 1.f, 1.5f);
-        mat(RT_LAMBERT, static_cast<float>(.64), static_cast<float>(.8), static_cast<float>(.0), 0.f);
-        sph(0.f, 1.f, 0.f, 1.f, 0);
-        sph(0.f, -1000.125f, 0.f, 1000.f, 3);
-        sph(2.f, 1.f, 0.f, 1.f, 1);
-        sph(-2.f, 1.f, 0.f, 1.f, 2);
-        sph(-2.f, 1.f, 0.f, -.99f, 2);
-    }
-    // src/main.cxx:131-177 (namespace typo fixed). Draw order: type, center.x, center.z, then
-    // the material's draws; a type-3 sphere pushes no material, so it shares the index of the
-    // next pushed one and trailing ones are resolved by default materials (lambert, albedo 1).
-    void cuda_variant()  // src/CUDA/cuda_impl.cu:425-437
-    {
-        mat(RT_LAMBERT, static_cast<float>(.1), static_cast<float>(.2), static_cast<float>(.5), 0.f);
-        mat(RT_METAL, static_cast<float>(.8), static_cast<float>(.6), static_cast<float>(.2), 0.f);
-        mat(RT_DIELECTRIC, 1.f, 1.f, 1.f, 1.5f);
-        mat(RT_LAMBERT, static_cast<float>(.64), static_cast<float>(.8), static_cast<float>(.0), 0.f);
-        sph(0.f, 0.f, -1.f, .5f, 0);
-        sph(0.f, -100.5f, -1.f, 100.f, 3);
-        sph(1.f, 0.f, -1.f, .5f, 1);
-        sph(-1.f, 0.f, -1.f, .5f, 2);
-        sph(-1.f, 0.f, -1.f, -.499f, 2);
-    }
-    void huge(uint32_t seed)
-    {
-        simple();
-        std::mt19937 gen{seed};
-        std::uniform_int_distribution<int> rd_int{0, 3};
-        std::uniform_real_distribution<float> rd_real{0.f, 1.f};
-        for (int a = -11; a < 11; ++a) {
-            for (int b = -11; b < 11; ++b) {
-                const int type = rd_int(gen);
-                const float cx = .9f * rd_real(gen) + static_cast<float>(a);
-                const float cz = .9f * rd_real(gen) + static_cast<float>(b);
-                if (hlen(hv{cx, .2f, cz} - hv{0.f, 1.f, 0.f}) < 1.f) continue;
-                sph(cx, .2f, cz, .2f, static_cast<uint32_t>(m.size()));
-                if (type == 0) {
-                    const float r = rd_real(gen), g = rd_real(gen), bb = rd_real(gen);
-                    mat(RT_LAMBERT, r, g, bb, 0.f);
-                } else if (type == 1) {
-                    const float r = rd_real(gen), g = rd_real(gen), bb = rd_real(gen);
-                    const float rough = .5f * rd_real(gen);
-                    mat(RT_METAL, r, g, bb, rough);
-                } else if (type == 2) {
-                    const float r = rd_real(gen), g = rd_real(gen), bb = rd_real(gen);
-                    mat(RT_DIELECTRIC, r, g, bb, 1.5f);
-                }
-            }
-        }
-        uint32_t need = 0;
-        for (auto &x : s) need = std::max(need, x.material + 1u);
-        while (m.size() < need) mat(RT_LAMBERT, 1.f, 1.f, 1.f, 0.f);
-    }
-    int emit(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres, rt_material *materials,
-             uint32_t material_cap, uint32_t *n_materials) const
-    {
-        if (n_spheres) *n_spheres = static_cast<uint32_t>(s.size());
-        if (n_materials) *n_materials = static_cast<uint32_t>(m.size());
-        if (spheres) {
-            if (sphere_cap < s.size()) return fail(RT_ERR_CAPACITY, "scene: sphere buffer too small");
-            std::memcpy(spheres, s.data(), s.size() * sizeof(rt_sphere));
-        }
-        if (materials) {
-            if (material_cap < m.size()) return fail(RT_ERR_CAPACITY, "scene: material buffer too small");
-            std::memcpy(materials, m.data(), m.size() * sizeof(rt_material));
-        }
-        return RT_OK;
-    }
-};
 
-// ---- scene blob: always-tested list + spatial clusters -------------------
-struct blob_t {
-    std::vector<float> data;  // 16-byte units
-    uint32_t n_geo = 0, n_always = 0, n_clusters = 0, clus_offset = 0, n_clusters_real = 0;
-    uint32_t n_supers = 0, supers_offset = 0, shade_offset = 0;
-    float clus_pad = 0.f;
-    std::vector<uint32_t> always;  // sphere indices tested on every segment (not clustered)
-};
-
-constexpr float kPadRel = 1e-3f;      // must match RT_PAD_REL in rt_kernel.hip
-// Spheres per cluster: 16 (two blocks of 8); RT_CLUSTER_SIZE (4..64, multiple of 4) for A/B,
-// read when a scene is created.
-uint32_t cluster_max()
-{
-    const char *e = std::getenv("RT_CLUSTER_SIZE");
-    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 16ul;
-    return v >= 4 && v <= 64 && v % 4 == 0 ? static_cast<uint32_t>(v) : 16u;
-}
-
-void split_clusters(const rt_sphere *s, std::vector<uint32_t> ids, std::vector<std::vector<uint32_t>> &out)
-{
-    const uint32_t kClusterMax = cluster_max();
-    if (ids.size() <= kClusterMax) {
-        out.push_back(std::move(ids));
-        return;
-    }
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (uint32_t i : ids)
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = std::min(lo[a], s[i].center[a]);
-            hi[a] = std::max(hi[a], s[i].center[a]);
-        }
-    int ax = 0;
-    for (int a = 1; a < 3; ++a)
-        if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
-    // split at a multiple of the cluster size so leaves come out full
-    const size_t half = ((ids.size() / 2 + kClusterMax - 1) / kClusterMax) * kClusterMax;
-    const size_t mid = std::min(half, ids.size() - 1);
-    std::nth_element(ids.begin(), ids.begin() + mid, ids.end(), [&](uint32_t x, uint32_t y) {
-        return s[x].center[ax] < s[y].center[ax] || (s[x].center[ax] == s[y].center[ax] && x < y);
-    });
-    std::vector<uint32_t> left(ids.begin(), ids.begin() + mid), right(ids.begin() + mid, ids.end());
-    split_clusters(s, std::move(left), out);
-    split_clusters(s, std::move(right), out);
-}
-
-blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered)
-{
-    // three classes by |r| against the median: huge (> 64x, e.g. the ground) are tested on
-    // every segment; big (> 4x) and small are clustered separately so that one big sphere
-    // does not inflate the boxes of the small ones
-    std::vector<uint32_t> always, big, small;
-    if (clustered && n >= 2 * cluster_max()) {
-        std::vector<float> r(n);
-        for (uint32_t i = 0; i < n; ++i) r[i] = std::fabs(s[i].radius);
-        std::vector<float> sorted = r;
-        std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
-        const float med = sorted[n / 2];
-        for (uint32_t i = 0; i < n; ++i) {
-            const bool finite = std::isfinite(s[i].center[0]) && std::isfinite(s[i].center[1]) &&
-                                std::isfinite(s[i].center[2]) && std::isfinite(r[i]);
-            if (!finite || r[i] > 64.f * med) always.push_back(i);
-            else if (r[i] > 4.f * med) big.push_back(i);
-            else small.push_back(i);
-        }
-    } else {
-        for (uint32_t i = 0; i < n; ++i) always.push_back(i);
-    }
-    // clusters: the big ones, padded to a multiple of 4 (an empty slot never passes), then the
-    // small ones; each group of 4 consecutive clusters gets a level-2 box
-    std::vector<std::vector<uint32_t>> clusters;
-    if (!big.empty()) split_clusters(s, big, clusters);
-    while (clusters.size() % 4) clusters.emplace_back();
-    if (!small.empty()) split_clusters(s, small, clusters);
-    // clusters stay in the DFS order of the median-split tree: 4 consecutive clusters are a
-    // depth-2 subtree, spatially tight, and become one level-2 box
-
-    auto pad4 = [](uint32_t x) { return (x + 3u) & ~3u; };
-    std::vector<float> geo;
-    std::vector<uint32_t> sidx;
-    auto push = [&](const std::vector<uint32_t> &ids) {
-        const uint32_t base = static_cast<uint32_t>(sidx.size());
-        for (uint32_t i : ids) {
-            geo.insert(geo.end(), {s[i].center[0], s[i].center[1], s[i].center[2], s[i].radius * s[i].radius}); // raytracer.hxx:58
-            sidx.push_back(i);
-        }
-        while (sidx.size() < base + pad4(static_cast<uint32_t>(ids.size()))) {
-            geo.insert(geo.end(), {0.f, 0.f, 0.f, -INFINITY});  // never hits
-            sidx.push_back(0xffffffffu);
-        }
-        return base;
-    };
-    blob_t b;
-    push(always);
-    b.always = always;
-    b.n_always = static_cast<uint32_t>(always.size());  // tested with its exact count (padding after it)
-    std::vector<float> crec;
-    std::vector<float> boxes;  // per cluster lo/hi (6 floats), for the level-2 boxes
-    for (const auto &c : clusters) {
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (uint32_t i : c)
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = std::min(lo[a], s[i].center[a] - std::fabs(s[i].radius));
-                hi[a] = std::max(hi[a], s[i].center[a] + std::fabs(s[i].radius));
-            }
-        float C[3] = {0.f, 0.f, 0.f}, E[3] = {-1e30f, -1e30f, -1e30f};  // empty: no ray enters
-        float kc = 0.f;
-        if (!c.empty()) {
-            for (int a = 0; a < 3; ++a) {
-                C[a] = .5f * (lo[a] + hi[a]);
-                E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
-            }
-            kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
-            b.clus_pad = std::max(b.clus_pad, kc);
-        }
-        boxes.insert(boxes.end(), {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]});
-        const uint32_t start = push(c);
-        const uint32_t cnt = pad4(static_cast<uint32_t>(c.size()));
-        uint32_t packed = start | (cnt << 16);
-        float pf;
-        std::memcpy(&pf, &packed, 4);
-        crec.insert(crec.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
-    }
-    // 4 never-hitting entries after the last cluster: the transposed member tests read 16
-    // member slots and mask the ones past the cluster's count
-    for (int i = 0; i < 4; ++i) {
-        geo.insert(geo.end(), {0.f, 0.f, 0.f, -INFINITY});
-        sidx.push_back(0xffffffffu);
-    }
-    b.n_geo = static_cast<uint32_t>(sidx.size());
-    b.n_clusters = static_cast<uint32_t>(clusters.size());
-    b.n_clusters_real = b.n_clusters;
-    // pad to a multiple of 4 clusters (grouped box tests) with boxes no ray enters:
-    // negative extents make t_in > t_out whatever the ray
-    while (b.n_clusters % 4) {
-        uint32_t packed = static_cast<uint32_t>(sidx.size());  // count 0
-        float pf;
-        std::memcpy(&pf, &packed, 4);
-        crec.insert(crec.end(), {0.f, 0.f, 0.f, -1e30f, -1e30f, -1e30f, 0.f, pf});
-        ++b.n_clusters;
-    }
-    // layout in 16-byte units: geo | sidx (padded) | clusters
-    b.data = geo;
-    if (b.data.empty()) b.data.assign(4, 0.f);
-    std::vector<uint32_t> sp = sidx;
-    while (sp.size() % 4) sp.push_back(0xffffffffu);
-    for (uint32_t v : sp) {
-        float f;
-        std::memcpy(&f, &v, 4);
-        b.data.push_back(f);
-    }
-    b.clus_offset = static_cast<uint32_t>(b.data.size() / 4);
-    b.data.insert(b.data.end(), crec.begin(), crec.end());
-    // level 2: one box over every 4 consecutive clusters (padding clusters contribute nothing)
-    b.supers_offset = static_cast<uint32_t>(b.data.size() / 4);
-    for (uint32_t g = 0; g < b.n_clusters; g += 4) {
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (uint32_t c = g; c < std::min(g + 4, b.n_clusters_real); ++c)
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = std::min(lo[a], boxes[6 * c + a]);
-                hi[a] = std::max(hi[a], boxes[6 * c + 3 + a]);
-            }
-        float C[3] = {0.f, 0.f, 0.f}, E[3] = {-1e30f, -1e30f, -1e30f};
-        float kc = 0.f;
-        if (lo[0] <= hi[0]) {
-            for (int a = 0; a < 3; ++a) {
-                C[a] = .5f * (lo[a] + hi[a]);
-                E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
-            }
-            kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
-            b.clus_pad = std::max(b.clus_pad, kc);
-        }
-        uint32_t packed = g | (4u << 16);
-        float pf;
-        std::memcpy(&pf, &packed, 4);
-        b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
-        ++b.n_supers;
-    }
-    // level 3: one box over every cluster (after the level-2 boxes)
-    {
-        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (uint32_t c = 0; c < b.n_clusters_real; ++c)
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = std::min(lo[a], boxes[6 * c + a]);
-                hi[a] = std::max(hi[a], boxes[6 * c + 3 + a]);
-            }
-        float C[3] = {0.f, 0.f, 0.f}, E[3] = {-1e30f, -1e30f, -1e30f};
-        float kc = 0.f;
-        if (lo[0] <= hi[0]) {
-            for (int a = 0; a < 3; ++a) {
-                C[a] = .5f * (lo[a] + hi[a]);
-                E[a] = std::max(hi[a] - C[a], C[a] - lo[a]);
-            }
-            kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
-            b.clus_pad = std::max(b.clus_pad, kc);
-        }
-        uint32_t packed = 0;
-        float pf;
-        std::memcpy(&pf, &packed, 4);
-        b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});
-    }
-    return b;
-}
-
-// The walk shortcut of dielectric spheres (rt_kernel.hip hint_candidate): a lane whose last hit
-// was such a sphere S, whose next segment (0, 1.002 t] up to S's candidate t lies in the ball
-// B(C, R_k) (R_k^2 = fl(fl(r r) kIsoR2Grow), the kernel's check of both ends), tests S's
-// neighbours instead of walking the clusters. The neighbours N(S) are the clustered spheres
-// T != S whose AABB, grown by the walk's own box pad for any origin in the ball, meets the ball;
-// for every other T the segment misses every padded box the walk would test, and the walk's
-// culling argument (such a T's candidate cannot beat t) holds sphere by sphere.
-// So the minimum over S, N(S) and the always-tested spheres (the ground, tested anyway) is the
-// walk's. R adds to R_k a margin for the float rounding of the kernel's check (a few ulp of
-// |C| + r). Per sphere: kShortcut | (geo slot of neighbour 0, + 1) | (slot of neighbour 1, + 1)
-// << 15 for spheres with at most two neighbours ("isolated": none), 0 otherwise.
-// O(dielectric x clustered spheres) once per scene.
-std::vector<uint32_t> shortcut_words(const rt_sphere *s, uint32_t n, const rt_material *m, const blob_t &b)
-{
-    std::vector<uint32_t> word(n, 0);
-    if (b.n_clusters_real == 0) return word;  // no walk to skip
-    // geo slot of each clustered sphere (blob layout: geo [n_geo] then sidx [n_geo])
-    std::vector<uint32_t> slot(n, ~0u);
-    for (uint32_t g = 0; g < b.n_geo; ++g) {
-        uint32_t id;
-        std::memcpy(&id, &b.data[4u * b.n_geo + g], 4);
-        if (id < n && g >= b.n_always) slot[id] = g;
-    }
-    const bool slots_fit = b.n_geo < 0x7fffu;
-    const char *e = std::getenv("RT_ISO_NB");  // RT_ISO_NB=0: isolated spheres only (A/B)
-    const bool nb_off = e && e[0] == '0';
-    std::vector<uint8_t> in_always(n, 0);
-    for (uint32_t i : b.always) in_always[i] = 1;
-    std::vector<uint32_t> others;
-    size_t n_diel = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (!in_always[i]) others.push_back(i);
-        if (m[s[i].material].kind == RT_DIELECTRIC) ++n_diel;
-    }
-    if (static_cast<double>(n_diel) * static_cast<double>(others.size()) > 4e8) return word;  // leave huge scenes alone
-    for (uint32_t S = 0; S < n && S < 0x7fffffffu; ++S) {
-        if (m[s[S].material].kind != RT_DIELECTRIC) continue;
-        const float r2 = s[S].radius * s[S].radius;  // the hint's geo entry, raytracer.hxx:58
-        const float r2k = r2 * rt::kIsoR2Grow;        // the kernel's check radius, squared
-        const double cx = s[S].center[0], cy = s[S].center[1], cz = s[S].center[2];
-        if (!std::isfinite(cx) || !std::isfinite(cy) || !std::isfinite(cz) || !std::isfinite(r2k)) continue;
-        const double rk = std::sqrt(static_cast<double>(r2k));
-        const double c1 = std::fabs(cx) + std::fabs(cy) + std::fabs(cz);
-        const double R = rk * (1.0 + 1e-5) + 1e-5 * (c1 + 2.0 * rk) + 1e-30;
-        const double pad = 1e-3 * (c1 + 2.0 * R) + static_cast<double>(b.clus_pad) + 1e-6;
-        const double C[3] = {cx, cy, cz};
-        uint32_t nb[2], n_nb = 0;
-        bool ok = true;
-        for (uint32_t T : others) {
-            if (T == S) continue;
-            const double rt_ = std::fabs(static_cast<double>(s[T].radius));
-            double d2 = 0.0;
-            for (int a = 0; a < 3; ++a) {
-                const double lo = s[T].center[a] - rt_ - pad, hi = s[T].center[a] + rt_ + pad;
-                const double e = C[a] < lo ? lo - C[a] : (C[a] > hi ? C[a] - hi : 0.0);
-                d2 += e * e;
-            }
-            if (!(d2 > R * R * (1.0 + 1e-9))) {
-                if (n_nb == 2 || !slots_fit || slot[T] == ~0u) {
-                    ok = false;
-                    break;
-                }
-                nb[n_nb++] = slot[T];
-            }
-        }
-        if (ok && n_nb && nb_off) ok = false;
-        if (ok)
-            word[S] = rt::kShortcut | (n_nb > 0 ? nb[0] + 1u : 0u) | (n_nb > 1 ? (nb[1] + 1u) << 15 : 0u);
-    }
-    return word;
-}
 
 uint32_t rows_of(const rt_params &p)
 {
@@ -685,46 +211,6 @@ int check_params(const rt_params *p)
     return RT_OK;
 }
 
-rt::UDiv make_udiv(uint32_t d)
-{
-    rt::UDiv r{0, 0, 0};
-    if (d <= 1) return r;  // d = 1: identity (t = 0, no shifts)
-    uint32_t l = 0;
-    while ((1ull << l) < d) ++l;
-    r.s1 = 1;
-    r.s2 = l - 1;
-    r.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1);
-    return r;
-}
-
-// Whether RN(a / b) == fma(fma(-q0, b, a), rb, q0) with rb = RN(1 / b), q0 = RN(a rb) for every
-// a = m (m in [2^23, 2^24), i.e. every float mantissa). Powers of two scale every step exactly,
-// so the identity then holds for every a >= 0 whose quotient and remainder stay normal: the
-// kernel's x / width and x / height (x = 0, a pixel index, or a canonical draw >= 2^-32) use
-// the two-FMA form when it holds. Checked once per divisor value (about 8 M host FMAs).
-bool exact_by_reciprocal(float b)
-{
-    static std::mutex mu;
-    static std::map<uint32_t, bool> cache;
-    uint32_t key;
-    std::memcpy(&key, &b, 4);
-    {
-        std::lock_guard<std::mutex> g(mu);
-        auto it = cache.find(key);
-        if (it != cache.end()) return it->second;
-    }
-    bool ok = std::isfinite(b) && b > 0.f && b >= 0x1p-60f && b <= 0x1p60f;
-    const float rb = 1.f / b;
-    for (uint32_t m = 1u << 23; ok && m < (1u << 24); ++m) {
-        const float a = static_cast<float>(m);
-        const float q0 = a * rb;
-        const float q = std::fma(std::fma(-q0, b, a), rb, q0);
-        ok = q == a / b;
-    }
-    std::lock_guard<std::mutex> g(mu);
-    cache[key] = ok;
-    return ok;
-}
 
 void fill_frame_consts(rt::KParams &k)
 {
@@ -755,22 +241,6 @@ void fill_frame_consts(rt::KParams &k)
     f.div_fast = (exact_by_reciprocal(f.fW) ? 1u : 0u) | (exact_by_reciprocal(f.fH) ? 2u : 0u);
 }
 
-// A passing cluster requested by at most RT_TRANSPOSE_MAX lanes (default 16, at most 16; 0 =
-// never) is tested transposed, (ray, member) pairs over the whole wave; same bits either way.
-uint32_t transpose_max_env()
-{
-    const char *e = std::getenv("RT_TRANSPOSE_MAX");
-    const unsigned long v = e && *e ? std::strtoul(e, nullptr, 10) : 16ul;
-    return static_cast<uint32_t>(std::min<unsigned long>(v, 16ul));
-}
-
-// Short exact root forms (rt_kernel.hip RayDiv) when the scene and the camera lie within 2^19 of
-// the origin; RT_FAST_ROOTS=0 keeps the IEEE sqrt/division sequences (A/B, tests); same bits.
-bool fast_roots_env()
-{
-    const char *e = std::getenv("RT_FAST_ROOTS");
-    return !(e && e[0] == '0');
-}
 bool camera_in_fast_range(const rt_camera &c)
 {
     for (int i = 0; i < 3; ++i)
@@ -779,58 +249,23 @@ bool camera_in_fast_range(const rt_camera &c)
     return std::fabs(c.lens_radius) <= 0x1p19f;
 }
 
-// RT_ROOT_BOX=0 disables the level-3 box gate (A/B); same bits either way.
-uint32_t root_box_env()
-{
-    const char *e = std::getenv("RT_ROOT_BOX");
-    return e && e[0] == '0' ? 0u : 1u;
-}
-
-// Deep-path split (render_kernel): paths that have traced RT_DEEP_SPLIT segments continue in a
-// second launch of the same kernel that deals them densely (0 = no split). Same bits either way.
-uint32_t deep_split_env()
-{
-    const char *e = std::getenv("RT_DEEP_SPLIT");
-    return e && *e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : kDeepSplitDefault;
-}
 // deep queue of a pass: 8 regions of 1/1024 of its samples each (at least 512): 0.8% of the
 // samples, where 0.2-0.3% reach the split depth on config 3; paths past a full region stay in the
-// main launch. A pass of fewer than RT_DEEP_MIN_ITEMS samples (default 2^25) issued while no
+// main launch. A pass of fewer than rt_options.deep_min_items samples (2^25) issued while no
 // other render runs (a lone frame) is not split: its deep launch would be a serial tail of
 // about max_depth - split iterations, which such a pass's own drain does not outweigh (config
 // 3's 8-way row share alone: 1.28-1.30 ms split vs 1.03-1.10). Passes issued while others run
 // (a frame stream) are split at any size: the unsplit drain costs issue (the 8-way share ran
 // 42% more VALU instructions per sample than the full frame) and the deep launches run beside
 // the other frames (8-way share, 7 streams: 0.50-0.51 ms per frame vs 0.58-0.59 unsplit).
-uint32_t deep_region_cap(uint32_t n_items)
+uint32_t deep_region_cap(uint64_t n_items)
 {
-    const char *e = std::getenv("RT_DEEP_REGION_DIV");
-    const unsigned long div = e && *e ? std::max(1ul, std::strtoul(e, nullptr, 10)) : 1024ul;
-    return std::max<uint32_t>(512u, static_cast<uint32_t>(n_items / div));
+    return static_cast<uint32_t>(std::max<uint64_t>(512u, n_items / 1024u));
 }
-// The deep launch's waves take the highest issue priority (RT_DEEP_PRIO=0 turns it off, A/B):
-// its paths are chains of ~56 dependent iterations, and beside other renders' waves each
-// iteration waits for the SIMD's other waves. Config 3's 8-way row share, split, 7 streams:
-// 0.513-0.515 ms vs 0.569-0.571 (profiles/r03/ab/deep_prio.txt); the full frame alike.
-uint32_t deep_prio_env()
+size_t deep_px_bytes(uint64_t n_pixels) { return (n_pixels + 255u) & ~static_cast<size_t>(255u); }
+size_t deep_queue_bytes(uint64_t n_pixels, uint64_t n_items)
 {
-    const char *e = std::getenv("RT_DEEP_PRIO");
-    return e && e[0] == '0' ? 0u : 1u;
-}
-
-// RT_ISO=0 turns off the isolated-sphere shortcut of the cluster walk (rt_kernel.hip
-// hint_candidate; A/B and tests; default on)
-uint32_t iso_env()
-{
-    const char *e = std::getenv("RT_ISO");
-    return e && e[0] == '0' ? 0u : 1u;
-}
-
-// RT_DEEP_ROOT_BOX=1 keeps the level-3 box gate in the deep launch (A/B; default off)
-bool deep_root_box_env()
-{
-    const char *e = std::getenv("RT_DEEP_ROOT_BOX");
-    return e && e[0] == '1';
+    return deep_px_bytes(n_pixels) + static_cast<size_t>(8u) * deep_region_cap(n_items) * 52u;
 }
 // a nonzero key of the camera basis and the depth limit (FNV-1a over their bytes)
 unsigned long long camera_key(const rt_camera &c, uint32_t max_depth)
@@ -843,11 +278,6 @@ unsigned long long camera_key(const rt_camera &c, uint32_t max_depth)
     mix(&max_depth, sizeof(max_depth));
     return h ? h : 1ull;
 }
-uint64_t deep_min_items_env()
-{
-    const char *e = std::getenv("RT_DEEP_MIN_ITEMS");
-    return e && *e ? std::strtoull(e, nullptr, 10) : (1ull << 25);
-}
 
 } // namespace
 
@@ -859,74 +289,27 @@ namespace {
 int render_compat(rt_scene *sc, const rt_camera *camera, const rt_params &P, float *d_rgb, hipStream_t st,
                   uint64_t *d_segments);
 
-// Render passes in flight: RT_PIPELINE=0 (or 1) runs the render kernels on the caller stream;
-// 2..kMaxBufs rotate that many internal streams. Default: one stream fewer than the process's
-// hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4; the caller's stream takes one), 2..4.
+// Render streams (rt_options.render_streams): 1 runs the render kernels on the caller stream;
+// 2..kMaxBufs rotate that many internal streams. 0 (auto): one stream fewer than the process's
+// hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4; the caller's stream takes one), 2..7.
 // The max-depth paths give every launch a drain of ~64 iterations whatever its size; with 3
 // streams (and partial grids, grid_wg_per_cu) two other renders fill the machine while one
 // drains. Measured on config 3 (frame stream): 3.81-3.87 ms/frame with 3 streams vs 3.90-3.93
-// with 2; an 8-way row share (14.7 M samples) 0.63-0.64 vs 0.68; 4 streams on 8 hardware
-// queues: 3.83-3.84 and 0.61. More streams than hardware queues share queues and serialise.
-uint32_t pipeline_env()
+// with 2; an 8-way row share (14.7 M samples) 0.63-0.64 vs 0.68. Round 3, with row shares split
+// in flight: 7 streams beat 4 (config 3's 8-way share 0.50 vs 0.58 ms, 4-way 0.88 vs 0.95; the
+// full frame 2.99-3.04 vs 3.06-3.08) and 8 (on 12 hardware queues) is slower again
+// (profiles/r03/ab). More streams than hardware queues share queues and serialise.
+uint32_t render_streams_of(const rt_options &o)
 {
-    const char *e = std::getenv("RT_PIPELINE");
-    if (!e || !*e) {
+    if (o.render_streams) return o.render_streams;
+    static const uint32_t hw_streams = [] {
         const char *q = std::getenv("GPU_MAX_HW_QUEUES");
         const unsigned long hw = q && *q ? std::strtoul(q, nullptr, 10) : 4ul;
-        // at most 7: with row shares split (passes in flight) 7 streams beat 4 (config 3's 8-way
-        // share 0.50 vs 0.58 ms, 4-way 0.88 vs 0.95; the full frame 2.99-3.04 vs 3.06-3.08) and
-        // 8 (on 12 hardware queues) is slower again (profiles/r03/ab); each stream holds two
-        // slot workspaces
         return static_cast<uint32_t>(std::clamp<unsigned long>(hw > 1 ? hw - 1 : 1, 2, 7));
-    }
-    const unsigned long v = std::strtoul(e, nullptr, 10);
-    return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxBufs));
+    }();
+    return hw_streams;
 }
 
-// Workspaces per internal stream (RT_WS_PER_STREAM, 1..2; default 2). Pass p renders on stream
-// p % streams into workspace p % (streams x this): with 2, the render that next takes a stream
-// waits only for that stream's previous render (stream order), not for the accumulation of
-// the pass that last used its workspace, which runs on the caller stream and, beside the
-// running renders, waits for free CU slots.
-uint32_t ws_per_stream_env()
-{
-    const char *e = std::getenv("RT_WS_PER_STREAM");
-    if (!e || !*e) return 2u;
-    const unsigned long v = std::strtoul(e, nullptr, 10);
-    return v <= 1 ? 1u : static_cast<uint32_t>(std::min<unsigned long>(v, kMaxWs / kMaxBufs));
-}
-
-// RT_DEBUG_STATS=1 selects the diagnostic instantiation (same bits, extra counters).
-bool debug_stats()
-{
-    const char *e = std::getenv("RT_DEBUG_STATS");
-    return e && e[0] == '1';
-}
-
-// RT_SHADE_LDS=0/1 forces the shading records out of / into LDS (-1 = automatic).
-int shade_lds_env()
-{
-    const char *e = std::getenv("RT_SHADE_LDS");
-    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-}
-
-// the render kernels' static LDS (per-wave transposed-test records 4 x 640 B, per-lane pending
-// normal 256 x 16 B, hint index and shortcut word 2 x 256 x 4 B: 8704 B), with a margin
-constexpr size_t kRenderStaticLds = 12u << 10;
-
-// RT_DEEP_SHADE_LDS=0 keeps the deep launch's shading records in global memory (A/B; default 1)
-bool deep_shade_lds_env()
-{
-    const char *e = std::getenv("RT_DEEP_SHADE_LDS");
-    return !(e && e[0] == '0');
-}
-
-// RT_VERBOSE=1 prints each launch's plan (variant, LDS bytes, occupancy, grid, items) to stderr.
-bool verbose()
-{
-    const char *e = std::getenv("RT_VERBOSE");
-    return e && e[0] == '1';
-}
 
 int ensure(void **ptr, size_t *have, size_t want)
 {
@@ -942,33 +325,14 @@ int ensure(void **ptr, size_t *have, size_t want)
     return RT_OK;
 }
 
+// frees every workspace of a scene (slots, deep queues, multi-pass sums, wavefront queues)
+// after the device is idle: the next render re-cuts them under max_workspace_bytes
+int free_workspaces(rt_scene *sc);
+
 } // namespace
 
 extern "C" {
 
-int rt_scene_simple(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres, rt_material *materials,
-                    uint32_t material_cap, uint32_t *n_materials)
-{
-    scene_builder b;
-    b.simple();
-    return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
-}
-
-int rt_scene_cuda(rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres, rt_material *materials,
-                  uint32_t material_cap, uint32_t *n_materials)
-{
-    scene_builder b;
-    b.cuda_variant();
-    return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
-}
-
-int rt_scene_huge(uint32_t seed, rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres,
-                  rt_material *materials, uint32_t material_cap, uint32_t *n_materials)
-{
-    scene_builder b;
-    b.huge(seed);
-    return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
-}
 
 int rt_scene_destroy(rt_scene *sc)
 {
@@ -1003,9 +367,22 @@ int rt_scene_destroy(rt_scene *sc)
 int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
                     uint32_t n_materials, int device, rt_scene **out)
 {
+    return rt_scene_create_ex(spheres, n_spheres, materials, n_materials, device, nullptr, out);
+}
+
+int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
+                       uint32_t n_materials, int device, const rt_options *options, rt_scene **out)
+{
     if (!out || (n_spheres && !spheres) || !materials || !n_materials)
         return fail(RT_ERR_INVALID, "rt_scene_create: null argument or no materials");
     *out = nullptr;
+    rt_options opt;
+    if (options) {
+        if (int rc = check_options(*options); rc) return rc;
+        opt = *options;
+    } else if (int rc = default_options(opt); rc) {
+        return rc;
+    }
     for (uint32_t i = 0; i < n_spheres; ++i)
         if (spheres[i].material >= n_materials)
             return fail(RT_ERR_INVALID, "rt_scene_create: sphere " + std::to_string(i) + " has material index " +
@@ -1027,8 +404,10 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         h[4] = mt.albedo[0]; h[5] = mt.albedo[1]; h[6] = mt.albedo[2]; h[7] = mt.param;
         std::memcpy(h + 8, &mt.kind, 4);
     }
-    blob_t blobs[2] = {build_blob(spheres, n_spheres, false), build_blob(spheres, n_spheres, true)};
-    const std::vector<uint32_t> shortcut = shortcut_words(spheres, n_spheres, materials, blobs[1]);
+    blob_t blobs[2] = {build_blob(spheres, n_spheres, false, opt.cluster_size),
+                       build_blob(spheres, n_spheres, true, opt.cluster_size)};
+    const std::vector<uint32_t> shortcut =
+        shortcut_words(spheres, n_spheres, materials, blobs[1], (opt.diag & RT_DIAG_NO_NEIGHBOURS) != 0);
     // shading records join each blob (so they sit in LDS next to the geometry): per original
     // sphere index {c, r}, {albedo, param}, then the material kinds as bytes, 16-B padded
     for (blob_t &b : blobs) {
@@ -1057,6 +436,7 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         }
     }
     rt_scene *sc = new rt_scene();
+    sc->opt = opt;
     for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
     sc->in_fast_range = true;
     for (uint32_t i = 0; i < n_spheres; ++i) {
@@ -1112,6 +492,10 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
             sc->max_lds = prop.sharedMemPerBlock;
         }
     }
+    if (rc == RT_OK) {
+        hipError_t e = rt::static_lds_render(rt::V_EXACT_LDS, 7, &sc->static_lds);
+        if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(e));
+    }
     for (uint32_t i = 0; rc == RT_OK && i < rt_scene::kRing; ++i) {
         hipEvent_t a = nullptr, b = nullptr;
         if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
@@ -1129,6 +513,32 @@ int rt_scene_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
     *out = sc;
     return RT_OK;
 }
+
+namespace {
+int free_workspaces(rt_scene *sc)
+{
+    RT_HIP(hipDeviceSynchronize());
+    auto drop = [](void *&p, size_t &n) -> hipError_t {
+        hipError_t e = hipSuccess;
+        if (p) e = hipFree(p);
+        p = nullptr;
+        n = 0;
+        return e;
+    };
+    for (uint32_t w = 0; w < kMaxWs; ++w) {
+        void *sp = sc->slots[w];
+        RT_HIP(drop(sp, sc->slots_bytes[w]));
+        sc->slots[w] = nullptr;
+        RT_HIP(drop(sc->deep[w], sc->deep_bytes[w]));
+        sc->deep_clean[w] = 0;
+    }
+    void *ap = sc->acc;
+    RT_HIP(drop(ap, sc->acc_bytes));
+    sc->acc = nullptr;
+    RT_HIP(drop(sc->wq, sc->wq_bytes));
+    return RT_OK;
+}
+} // namespace
 
 namespace {
 // Calls on one scene may come on different caller streams: order a call after everything the
@@ -1191,8 +601,10 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     if (n_pixels == 0) return RT_OK;
     if (n_pixels >= (1ull << 31)) return fail(RT_ERR_INVALID, "rt_render_device: more than 2^31 pixels in one call");
     k.n_pixels = static_cast<uint32_t>(n_pixels);
-    // 64-pixel tiles (one wave's lanes for one sample), 2^lw wide and 64/2^lw rows tall
-    k.tile_lw = tile_lw_for(P.width, k.row_stride);
+    // 64-pixel tiles (one wave's lanes for one sample), 8 x 8 (the kernel's decomposition takes
+    // 2^lw x 64/2^lw; 16x4, 32x2 and 64x1 measured alike or slower for strided row shares:
+    // 8-way share 0.61-0.62 ms at 8x8, 0.62 at 32x2, 0.66 at 64x1)
+    k.tile_lw = 3u;
     const uint32_t tw = 1u << k.tile_lw, th = 64u >> k.tile_lw;
     const bool tiled = (P.width % tw) == 0u;
     k.tiles_x = tiled ? P.width / tw : 1u;
@@ -1202,20 +614,22 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
 
 
     // Variant: exact (bit-exact) or fast (tolerance); clustered culling unless brute force is
-    // asked for; the scalar-cache A/B variant is brute force only. Each needs its blob in LDS.
+    // asked for; the scalar-cache A/B variant is brute force only. Each needs its blob in LDS
+    // next to the kernel's static LDS (sc->static_lds, the culled kernel's: the largest).
+    const rt_options &O = sc->opt;
     int variant = (P.flags & RT_FLAG_FAST_MATH) ? rt::V_FAST_LDS : rt::V_EXACT_LDS;
     bool cull = !(P.flags & RT_FLAG_BRUTE_FORCE) && sc->n_clusters[1] > 0;
     const bool wave = (P.flags & RT_FLAG_WAVEFRONT) != 0u;
     if (wave && (P.flags & (RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE)))
         return fail(RT_ERR_UNSUPPORTED, "rt_render_device: the wavefront variant is the exact kernel only");
     if (P.flags & RT_FLAG_SCALAR_SCENE) { variant = rt::V_EXACT_SCALAR; cull = false; }
-    if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->shade_offset[cull]) * 16u > sc->max_lds) {
+    if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->shade_offset[cull]) * 16u + sc->static_lds > sc->max_lds) {
         if (variant == rt::V_FAST_LDS || cull) return fail(RT_ERR_UNSUPPORTED, "rt_render_device: scene too large for LDS");
         variant = rt::V_EXACT_SCALAR;
     }
     if (wave && variant != rt::V_EXACT_LDS)
         return fail(RT_ERR_UNSUPPORTED, "rt_render_device: the wavefront variant needs the scene in LDS");
-    if (variant == rt::V_EXACT_LDS && debug_stats() && !wave) {
+    if (variant == rt::V_EXACT_LDS && (O.diag & RT_DIAG_STATS) && !wave) {
         variant = rt::V_STATS_LDS;
         if (!sc->dbg) {
             RT_HIP(hipMalloc((void **)&sc->dbg, rt::kDbgWords * sizeof(unsigned long long)));
@@ -1234,13 +648,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     k.clus_pad = sc->clus_pad[b];
     k.n_supers = sc->n_supers[b];
     k.supers_offset = sc->supers_offset[b];
-    k.use_root = root_box_env();
-    k.iso = iso_env();
-    k.transpose_max = transpose_max_env();
-    k.fast_roots = sc->in_fast_range && camera_in_fast_range(*camera) && fast_roots_env() ? 1u : 0u;
+    k.use_root = (O.diag & RT_DIAG_NO_ROOT_BOX) ? 0u : 1u;
+    k.iso = (O.diag & RT_DIAG_NO_SHORTCUT) ? 0u : 1u;
+    k.transpose_max = O.transpose_max;
+    k.fast_roots = sc->in_fast_range && camera_in_fast_range(*camera) && !(O.diag & RT_DIAG_IEEE_ROOTS) ? 1u : 0u;
     k.shade_offset = sc->shade_offset[b];
     // the shading records (the blob's tail) join the geometry in LDS unless that costs
-    // workgroups per CU; RT_SHADE_LDS=0/1 forces the choice for A/B
+    // workgroups per CU; RT_DIAG_SHADE_LDS / RT_DIAG_SHADE_GLOBAL force the choice (same bits)
     auto occ_for = [&](int in_lds, int *out) -> int {
         int &o = sc->occ[variant][cull ? 1 : 0][in_lds];
         if (o < 0) {
@@ -1254,27 +668,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     int occ_geo = 0, occ_all = 0;
     if (int rc = occ_for(0, &occ_geo); rc) return rc;
     if (int rc = occ_for(1, &occ_all); rc) return rc;
-    const int force = shade_lds_env();
-    k.shade_lds = variant != rt::V_EXACT_SCALAR && static_cast<size_t>(k.blob_units) * 16u <= sc->max_lds &&
-                  (force >= 0 ? force == 1 : occ_all >= occ_geo);
+    const bool shade_fits = static_cast<size_t>(k.blob_units) * 16u + sc->static_lds <= sc->max_lds;
+    k.shade_lds = variant != rt::V_EXACT_SCALAR && shade_fits &&
+                  ((O.diag & RT_DIAG_SHADE_LDS) ? true : (O.diag & RT_DIAG_SHADE_GLOBAL) ? false : occ_all >= occ_geo);
     k.lds_units = variant == rt::V_EXACT_SCALAR ? 0u : (k.shade_lds ? k.blob_units : k.shade_offset);
     const size_t lds = static_cast<size_t>(k.lds_units) * 16u;
     const int occ = k.shade_lds ? occ_all : occ_geo;
 
-    // pass planning: the slot workspace of one pass (12 B per sample and pixel) stays under
-    // the budget; passes hold a multiple of 4 samples so no reduce block straddles two
-    const uint64_t per_sample = n_pixels * 12ull;
-    uint64_t spp_pass = std::min<uint64_t>(P.spp, slot_budget() / per_sample);
-    spp_pass = std::min<uint64_t>(spp_pass, ((1ull << 31) - 8192) / n_pixels);  // items fit 31 bits
-    if (spp_pass < P.spp) spp_pass &= ~3ull;
-    if (spp_pass == 0) spp_pass = 4;
-    if (n_pixels * std::min<uint64_t>(spp_pass, P.spp) >= (1ull << 31) - 8192)
-        return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
-    // frames in flight: render pass p runs on internal stream xs[p % bufs] with workspace
-    // w = p % n_ws, ordered after that stream's previous render and after the caller-stream
-    // work that last read workspace w (the accumulation of pass p - n_ws); render kernels
-    // touch no caller memory, so the caller stream sees the same results in the same order.
-    // RT_PIPELINE=0: everything on the caller stream.
     // deep-path split, unless a pass with this camera (and depth limit) has overflowed the deep
     // queue on this scene: paths that long are common there (the corrected camera: 8.4% of the
     // samples pass 8 segments, 59% of the segments), and a partial split only adds a tail
@@ -1294,23 +694,86 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     const unsigned long long deep_key = camera_key(*camera, P.max_depth);
     const bool deep_off = std::find_if(sc->deep_off.begin(), sc->deep_off.end(),
                                        [&](const auto &e) { return e.first == deep_key; }) != sc->deep_off.end();
-    const uint32_t deep_split = deep_off ? 0u : deep_split_env();
-    const uint64_t deep_min_items = deep_min_items_env();
-    const uint32_t bufs = wave ? 1u : pipeline_env();  // the wavefront variant: caller stream only
+    const uint32_t deep_split = deep_off ? 0u : O.deep_split;
+    // culled scenes only: with a handful of spheres (the simple scene, brute force) a deep
+    // segment is cheap and the deep launch's overhead outweighs the drain it saves
+    // (config 2: 0.98-1.00 vs 0.98-0.99 ms per frame)
+    const bool may_split = deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth;
+
+    // Pass planning. The slot workspace of one pass (12 B per sample and pixel) stays within
+    // max_pass_bytes; passes hold a multiple of 4 samples so no reduce block straddles two.
+    // Frames in flight: render pass p runs on internal stream xs[p % bufs] with workspace
+    // w = p % n_ws, ordered after that stream's previous render and after the caller-stream
+    // work that last read workspace w (the accumulation of pass p - n_ws); render kernels
+    // touch no caller memory, so the caller stream sees the same results in the same order.
+    // One stream: everything on the caller stream. Under max_workspace_bytes the passes shrink
+    // first (frames in flight are what keeps the machine full), then the workspaces per
+    // stream, then the streams; the bits never depend on the cut.
+    const uint64_t per_sample = n_pixels * 12ull;
+    const uint64_t items_cap = ((1ull << 31) - 8192) / n_pixels;  // items fit 31 bits
+    uint64_t spp_full = std::min<uint64_t>({P.spp, O.max_pass_bytes / per_sample, items_cap});
+    if (spp_full < P.spp) spp_full &= ~3ull;
+    if (spp_full == 0) spp_full = 4;
+    if (n_pixels * std::min<uint64_t>(spp_full, P.spp) >= (1ull << 31) - 8192)
+        return fail(RT_ERR_INVALID, "rt_render_device: too many pixels in one call");
+    auto wave_cap = [&](uint64_t sp) {
+        return static_cast<uint32_t>(std::min<uint64_t>(n_pixels * std::min<uint64_t>(sp, P.spp), O.wave_queue_rays));
+    };
+    auto n_ws_of = [](uint32_t streams, uint32_t wsps) { return streams > 1 ? streams * wsps : 1u; };
+    auto footprint = [&](uint32_t streams, uint32_t wsps, uint64_t sp) -> uint64_t {
+        const uint64_t spe = std::min<uint64_t>(sp, P.spp);
+        uint64_t t = static_cast<uint64_t>(n_ws_of(streams, wsps)) *
+                     (per_sample * spe + (may_split ? deep_queue_bytes(n_pixels, n_pixels * spe) : 0u));
+        if (sp < P.spp) t += per_sample;  // the multi-pass sums
+        if (wave) t += 2ull * wave_cap(sp) * 52u + 512u;
+        return t;
+    };
+    uint32_t bufs = wave ? 1u : render_streams_of(O);  // the wavefront variant: caller stream only
+    uint32_t wsps = O.workspaces_per_stream;
+    uint64_t spp_pass = spp_full;
+    if (const uint64_t cap = O.max_workspace_bytes) {
+        while (footprint(bufs, wsps, spp_pass) > cap) {
+            if (spp_pass > 4) {
+                spp_pass = std::max<uint64_t>(4, (std::min<uint64_t>(spp_pass, P.spp) - 1) & ~3ull);
+                continue;
+            }
+            spp_pass = spp_full;
+            if (bufs > 1 && wsps > 1) wsps = 1;
+            else if (bufs > 1) --bufs;
+            else return fail(RT_ERR_CAPACITY, "rt_render_device: max_workspace_bytes " + std::to_string(cap) +
+                                                  " below one 4-sample pass of this frame (" +
+                                                  std::to_string(footprint(1, 1, 4)) + " bytes)");
+        }
+    }
     const bool pipe = bufs > 1;
-    const uint32_t n_ws = pipe ? bufs * ws_per_stream_env() : 1u;
+    const uint32_t n_ws = n_ws_of(bufs, wsps);
+    const uint64_t spe = std::min<uint64_t>(spp_pass, P.spp);
+    // under a cap, workspaces left larger (or more numerous) by earlier frames are re-cut once
+    if (O.max_workspace_bytes) {
+        uint64_t after = 0;
+        for (uint32_t w = 0; w < kMaxWs; ++w) {
+            after += w < n_ws ? std::max<uint64_t>(sc->slots_bytes[w], per_sample * spe) : sc->slots_bytes[w];
+            after += w < n_ws && may_split ? std::max<uint64_t>(sc->deep_bytes[w], deep_queue_bytes(n_pixels, n_pixels * spe))
+                                           : sc->deep_bytes[w];
+        }
+        after += spp_pass < P.spp ? std::max<uint64_t>(sc->acc_bytes, per_sample) : sc->acc_bytes;
+        after += wave ? std::max<uint64_t>(sc->wq_bytes, 2ull * wave_cap(spp_pass) * 52u + 512u) : sc->wq_bytes;
+        if (after > O.max_workspace_bytes)
+            if (int rc = free_workspaces(sc); rc) return rc;
+    }
+    sc->used_streams = bufs;
+    sc->used_ws = n_ws;
+    sc->used_pass = static_cast<uint32_t>(spe);
     if (spp_pass < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
     for (uint32_t w = 0; w < n_ws; ++w)
-        if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], per_sample * std::min<uint64_t>(spp_pass, P.spp)); rc)
-            return rc;
-    k.chunk_items = chunk_items();
+        if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], per_sample * spe); rc) return rc;
     // wavefront variant: two ray queues of cap rays (52 B each) and their counters
     uint32_t wcap = 0;
     rt::RayQueue wqa{}, wqb{};
     int wgrid = 0;
     if (wave) {
-        wcap = static_cast<uint32_t>(std::min<uint64_t>(n_pixels * std::min<uint64_t>(spp_pass, P.spp), wave_queue_env()));
+        wcap = wave_cap(spp_pass);
         const size_t qbytes = static_cast<size_t>(wcap) * 52u;
         if (int rc = ensure(&sc->wq, &sc->wq_bytes, 2 * qbytes + 512); rc) return rc;
         auto carve = [&](char *base, rt::RayQueue &q) {
@@ -1359,12 +822,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.sample_end = s1;
         fill_frame_consts(k);
         k.n_items = static_cast<uint32_t>(n_pixels * (s1 - s0));
-        {   // the last tail_pct % of the items go out in 64-item chunks (even end-of-launch drain)
-            const uint64_t tail = static_cast<uint64_t>(k.n_items) * tail_pct() / 100u;
-            k.n_big_chunks = static_cast<uint32_t>((k.n_items - tail) / k.chunk_items);
-            const uint32_t rest = k.n_items - k.n_big_chunks * k.chunk_items;
-            k.n_chunks = k.n_big_chunks + (rest + 63u) / 64u;
-        }
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
@@ -1373,19 +830,17 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.deep_depth = 0;
         k.deep_mode = 0;
         bool two_part = false;
-        // culled scenes only: with a handful of spheres (the simple scene, brute force) a deep
-        // segment is cheap and the deep launch's overhead outweighs the drain it saves
-        // (config 2: 0.98-1.00 vs 0.98-0.99 ms per frame)
-        if (deep_split && !wave && cull_mode == 7 && deep_split < P.max_depth && (k.n_items >= deep_min_items || in_flight)) {
+        if (may_split && (k.n_items >= O.deep_min_items || in_flight)) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
-            const size_t px_bytes = (n_pixels + 255u) & ~static_cast<size_t>(255u);
+            const size_t px_bytes = deep_px_bytes(n_pixels);
             void *had = sc->deep[wb];
-            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], px_bytes + static_cast<size_t>(cap) * 52u); rc) return rc;
+            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], deep_queue_bytes(n_pixels, k.n_items)); rc) return rc;
             if (sc->deep[wb] != had) sc->deep_clean[wb] = 0;  // new memory
-            if (sc->deep_clean[wb] < px_bytes) {  // flags over bytes a queue may have used
+            if (sc->deep_clean[wb] < px_bytes)  // flags over bytes a queue may have used
                 RT_HIP(hipMemsetAsync(sc->deep[wb], 0, px_bytes, xst));
-                sc->deep_clean[wb] = px_bytes;
-            }
+            // every accumulation clears the flags its pass set, and the bytes past px_bytes are
+            // this pass's queue storage: only the leading px_bytes are known to be zero after it
+            sc->deep_clean[wb] = px_bytes;
             char *base = static_cast<char *>(sc->deep[wb]);
             k.deep.px = reinterpret_cast<uint8_t *>(base);
             base += px_bytes;
@@ -1398,11 +853,11 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             k.deep_depth = deep_split;
             two_part = pipe && !in_flight;
         }
-        if (verbose())
-            std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u samples=[%u,%u) %s%u\n",
-                         variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1,
-                         k.guided_l2b < 0.f ? "guided log2(beta)*1e6=" : "chunk=",
-                         k.guided_l2b < 0.f ? static_cast<uint32_t>(-k.guided_l2b * 1e6f) : k.chunk_items);
+        if (O.diag & RT_DIAG_VERBOSE)
+            std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u "
+                                 "samples=[%u,%u) streams=%u workspaces=%u split=%u guided log2(beta)*1e6=%u\n",
+                         variant, cull_mode, k.shade_lds, lds, occ, sc->cu_count, grid, k.n_items, s0, s1, bufs, n_ws,
+                         k.deep_depth, static_cast<uint32_t>(-k.guided_l2b * 1e6f));
         if (wave) {
             // items in chunks of wcap: one generation launch, then max_depth bounce launches
             // (each takes every ray of its input queue; continuing rays go to the other queue)
@@ -1436,19 +891,22 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 // the deep paths bounce inside glass spheres, inside the box over all clusters:
                 // the level-3 gate only costs there (alike within box noise, fewer box tests;
                 // same bits)
-                kd.use_root = deep_root_box_env() ? k.use_root : 0u;
-                kd.deep_prio = deep_prio_env();
+                kd.use_root = 0u;
+                // its waves at the top issue priority: each path is a chain of ~56 dependent
+                // iterations, and beside other renders' waves every iteration waits for the
+                // SIMD's other waves (config 3's 8-way share, split, 7 streams: 0.513-0.515 ms vs
+                // 0.569-0.571; profiles/r03/ab/deep_prio.txt)
+                kd.deep_prio = 1u;
                 // the shading records in LDS for the deep launch of a pass issued alone: its
                 // paths bounce in glass and shade every segment, and its few busy waves wait on
                 // each global round trip (config 3 single frame: deep launch 0.59 vs 0.65 ms).
                 // Not beside other renders: its larger workgroups then displace theirs (frame
                 // stream 2.69-2.73 vs 2.57-2.59 ms per frame, 8-way share 0.45 vs 0.42)
-                if (deep_shade_lds_env() && !in_flight && variant != rt::V_EXACT_SCALAR && !k.shade_lds &&
-                    static_cast<size_t>(k.blob_units) * 16u + kRenderStaticLds <= sc->max_lds) {
+                if (!in_flight && variant != rt::V_EXACT_SCALAR && !k.shade_lds && shade_fits) {
                     kd.shade_lds = 1u;
                     kd.lds_units = k.blob_units;
                 }
-                if (variant == rt::V_STATS_LDS && std::getenv("RT_DEBUG_DEEP_ONLY")) {
+                if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) {
                     // diagnostics: the counters and events of the deep launch alone
                     RT_HIP(hipMemsetAsync(sc->dbg, 0, 16 * sizeof(unsigned long long), xst));
                     RT_HIP(hipMemsetAsync(sc->dbg + rt::kDbgEvBase, 0, rt::kDbgEvents * sizeof(unsigned long long), xst));
@@ -1590,6 +1048,25 @@ int rt_scene_kernel_times(rt_scene *sc, uint32_t max, float *ms, uint32_t *n)
         RT_HIP(hipEventElapsedTime(ms + i, sc->ev_begin[r], sc->ev_end[r]));
     }
     *n = cnt;
+    return RT_OK;
+}
+
+int rt_scene_usage_get(const rt_scene *sc, rt_scene_usage *out)
+{
+    if (!sc || !out) return fail(RT_ERR_INVALID, "rt_scene_usage_get: null argument");
+    rt_scene_usage u{};
+    uint64_t ws = sc->acc_bytes + sc->wq_bytes;
+    for (uint32_t w = 0; w < kMaxWs; ++w) ws += sc->slots_bytes[w] + sc->deep_bytes[w];
+    uint64_t fixed = kCtrWords * sizeof(uint32_t) + (sc->dbg ? rt::kDbgWords * sizeof(unsigned long long) : 0u);
+    for (int b = 0; b < 2; ++b) fixed += static_cast<uint64_t>(sc->blob_units[b]) * 16u;
+    u.device_bytes = ws + fixed;
+    u.workspace_bytes = ws;
+    u.render_streams = sc->used_streams;
+    u.workspaces = sc->used_ws;
+    u.pass_samples = sc->used_pass;
+    u.static_lds_bytes = static_cast<uint32_t>(sc->static_lds);
+    u.max_lds_bytes = static_cast<uint32_t>(sc->max_lds);
+    *out = u;
     return RT_OK;
 }
 
@@ -1754,6 +1231,104 @@ const rccl_api &rccl()
     }();
     return api;
 }
+
+// RT_DIAG_STANDIN_TRANSPORT: RCCL's point-to-point calls restated as stream-ordered device
+// copies between ranks that share one device, so that the RCCL gather branch of
+// rt_multi_render_device (grouped send/recv per peer on the ranks' streams, slot offsets, tile
+// reuse across frames in flight) runs on one GPU. Semantics kept: within a group, a send on
+// rank a's stream to peer b pairs with the receive on rank b's stream from a; the receive's
+// stream waits for the send stream's prior work, copies, and the send stream's later work
+// waits for the copy (the tile may not be overwritten before it has left), as with RCCL.
+namespace standin {
+struct comm { int rank, n, dev; };
+struct op { bool is_send; const void *src; void *dst; size_t bytes; int peer; comm *c; hipStream_t st; };
+thread_local std::vector<op> g_ops;
+thread_local int g_depth = 0;
+size_t type_bytes(ncclDataType_t t) { return t == ncclFloat ? 4u : t == ncclUint8 ? 1u : 0u; }
+ncclResult_t comm_init_all(ncclComm_t *comms, int n, const int *devs)
+{
+    for (int i = 0; i < n; ++i) comms[i] = reinterpret_cast<ncclComm_t>(new comm{i, n, devs ? devs[i] : i});
+    return ncclSuccess;
+}
+ncclResult_t comm_destroy(ncclComm_t c)
+{
+    delete reinterpret_cast<comm *>(c);
+    return ncclSuccess;
+}
+ncclResult_t push(bool is_send, const void *src, void *dst, size_t count, ncclDataType_t t, int peer, ncclComm_t c,
+                  hipStream_t st)
+{
+    comm *cc = reinterpret_cast<comm *>(c);
+    if (!cc || !type_bytes(t) || peer < 0 || peer >= cc->n || peer == cc->rank) return ncclInvalidArgument;
+    g_ops.push_back({is_send, src, dst, count * type_bytes(t), peer, cc, st});
+    return g_depth ? ncclSuccess : ncclInvalidUsage;  // only grouped calls are emulated
+}
+ncclResult_t send(const void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t c, hipStream_t st)
+{
+    return push(true, buf, nullptr, count, t, peer, c, st);
+}
+ncclResult_t recv(void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t c, hipStream_t st)
+{
+    return push(false, nullptr, buf, count, t, peer, c, st);
+}
+ncclResult_t group_start()
+{
+    ++g_depth;
+    return ncclSuccess;
+}
+ncclResult_t group_end()
+{
+    if (g_depth <= 0) return ncclInvalidUsage;
+    if (--g_depth) return ncclSuccess;
+    std::vector<op> ops;
+    ops.swap(g_ops);
+    std::vector<bool> used(ops.size(), false);
+    ncclResult_t res = ncclSuccess;
+    for (size_t i = 0; i < ops.size() && res == ncclSuccess; ++i) {
+        if (!ops[i].is_send) continue;
+        const op &sd = ops[i];
+        size_t j = 0;
+        for (; j < ops.size(); ++j)
+            if (!used[j] && !ops[j].is_send && ops[j].c->rank == sd.peer && ops[j].peer == sd.c->rank) break;
+        if (j == ops.size() || ops[j].bytes != sd.bytes) {
+            res = ncclInvalidUsage;
+            break;
+        }
+        used[i] = used[j] = true;
+        const op &rv = ops[j];
+        hipEvent_t sent = nullptr, landed = nullptr;
+        if (hipEventCreateWithFlags(&sent, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&landed, hipEventDisableTiming) != hipSuccess || hipEventRecord(sent, sd.st) != hipSuccess ||
+            hipStreamWaitEvent(rv.st, sent, 0) != hipSuccess ||
+            hipMemcpyAsync(rv.dst, sd.src, sd.bytes, hipMemcpyDeviceToDevice, rv.st) != hipSuccess ||
+            hipEventRecord(landed, rv.st) != hipSuccess || hipStreamWaitEvent(sd.st, landed, 0) != hipSuccess)
+            res = ncclUnhandledCudaError;
+        if (sent) (void)hipEventDestroy(sent);
+        if (landed) (void)hipEventDestroy(landed);
+    }
+    for (size_t i = 0; i < ops.size() && res == ncclSuccess; ++i)
+        if (!used[i]) res = ncclInvalidUsage;  // a receive without its send
+    return res;
+}
+const char *error_string(ncclResult_t r) { return r == ncclSuccess ? "success" : "stand-in transport: unmatched or failed call"; }
+} // namespace standin
+
+const rccl_api &standin_api()
+{
+    static rccl_api api = [] {
+        rccl_api a;
+        a.comm_init_all = standin::comm_init_all;
+        a.comm_destroy = standin::comm_destroy;
+        a.send = standin::send;
+        a.recv = standin::recv;
+        a.group_start = standin::group_start;
+        a.group_end = standin::group_end;
+        a.error_string = standin::error_string;
+        a.ok = true;
+        return a;
+    }();
+    return api;
+}
 } // namespace
 
 // Persistent multi-GPU context (rt_multi_*): rank r of N renders the rows y = r, r + N, ...
@@ -1770,6 +1345,7 @@ struct rt_multi {
     int n = 0;
     std::vector<int> dev;
     bool rccl = false;  // every rank on its own device: gather over RCCL
+    const rccl_api *api = nullptr;  // RCCL, or the stand-in (RT_DIAG_STANDIN_TRANSPORT)
     std::vector<rt_scene *> sc;
     std::vector<hipStream_t> st;        // rank r > 0: its stream (rank 0 runs on the caller's stream)
     std::vector<ncclComm_t> comm;
@@ -1819,35 +1395,51 @@ extern "C" {
 int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
                     const int *devices, int n_ranks, rt_multi **out)
 {
+    return rt_multi_create_ex(spheres, n_spheres, materials, n_materials, devices, n_ranks, nullptr, out);
+}
+
+int rt_multi_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
+                       const int *devices, int n_ranks, const rt_options *options, rt_multi **out)
+{
     if (!out) return fail(RT_ERR_INVALID, "rt_multi_create: null output");
     *out = nullptr;
+    rt_options opt;
+    if (options) {
+        if (int rc = check_options(*options); rc) return rc;
+        opt = *options;
+    } else if (int rc = default_options(opt); rc) {
+        return rc;
+    }
+    // two supported layouts: every rank on its own device (RCCL), or every rank on rank 0's
+    // device (virtual ranks); a mix would gather through cross-device copies no test covers.
+    // Checked before any HIP call.
+    bool distinct = true, all_same = true;
+    if (devices && n_ranks > 0) {
+        if (n_ranks > 64) return fail(RT_ERR_INVALID, "rt_multi_create: at most 64 ranks");
+        for (int r = 1; r < n_ranks; ++r) {
+            all_same = all_same && devices[r] == devices[0];
+            for (int q = 0; q < r; ++q) distinct = distinct && devices[q] != devices[r];
+        }
+        if (!distinct && !all_same)
+            return fail(RT_ERR_INVALID, "rt_multi_create: devices must be all distinct or all rank 0's device");
+    }
+    const bool standin = (opt.diag & RT_DIAG_STANDIN_TRANSPORT) != 0u;
+    if (standin && !(devices && n_ranks > 1 && all_same))
+        return fail(RT_ERR_INVALID, "rt_multi_create: the stand-in transport needs two or more ranks on one device");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_DEVICE, "rt_multi_create: no HIP device");
     const int N = n_ranks <= 0 ? ndev : n_ranks;
     if (!devices && N > ndev) return fail(RT_ERR_INVALID, "rt_multi_create: more ranks than devices (pass a device list)");
     if (N > 64) return fail(RT_ERR_INVALID, "rt_multi_create: at most 64 ranks");
-    rt_multi *m = new rt_multi();
-    m->n = N;
     for (int r = 0; r < N; ++r) {
         const int d = devices ? devices[r] : r;
-        if (d < 0 || d >= ndev) {
-            delete m;
-            return fail(RT_ERR_INVALID, "rt_multi_create: bad device index");
-        }
-        m->dev.push_back(d);
+        if (d < 0 || d >= ndev) return fail(RT_ERR_INVALID, "rt_multi_create: bad device index");
     }
-    // two supported layouts: every rank on its own device (RCCL), or every rank on rank 0's
-    // device (virtual ranks); a mix would gather through cross-device copies no test covers
-    bool distinct = true, all_same = true;
-    for (int r = 1; r < N; ++r) {
-        all_same = all_same && m->dev[r] == m->dev[0];
-        for (int q = 0; q < r; ++q) distinct = distinct && m->dev[q] != m->dev[r];
-    }
-    if (!distinct && !all_same) {
-        delete m;
-        return fail(RT_ERR_INVALID, "rt_multi_create: devices must be all distinct or all rank 0's device");
-    }
-    m->rccl = N > 1 && distinct;
+    rt_multi *m = new rt_multi();
+    m->n = N;
+    for (int r = 0; r < N; ++r) m->dev.push_back(devices ? devices[r] : r);
+    m->rccl = N > 1 && (distinct || standin);
+    m->api = standin ? &standin_api() : &rccl();
     m->sc.assign(N, nullptr);
     m->st.assign(N, nullptr);
     m->tile.assign(N, nullptr);
@@ -1862,7 +1454,7 @@ int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         return rc == RT_OK;
     };
     for (int r = 0; r < N && rc == RT_OK; ++r) {
-        rc = rt_scene_create(spheres, n_spheres, materials, n_materials, m->dev[r], &m->sc[r]);
+        rc = rt_scene_create_ex(spheres, n_spheres, materials, n_materials, m->dev[r], &opt, &m->sc[r]);
         if (rc != RT_OK) break;
         chk(hipSetDevice(m->dev[r]), "hipSetDevice");
         if (r > 0) chk(hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking), "hipStreamCreate");
@@ -1877,7 +1469,7 @@ int rt_multi_create(const rt_sphere *spheres, uint32_t n_spheres, const rt_mater
         chk(hipEventCreate(&m->ev_t1), "hipEventCreate");
     }
     if (rc == RT_OK && m->rccl) {
-        const rccl_api &api = rccl();
+        const rccl_api &api = *m->api;
         if (!api.ok) {
             rc = fail(RT_ERR_COMM, "rt_multi_create: librccl.so.1 not loadable");
         } else {
@@ -1905,7 +1497,7 @@ int rt_multi_destroy(rt_multi *m)
     (void)hipSetDevice(m->dev[0]);
     (void)hipDeviceSynchronize();
     for (auto c : m->comm)
-        if (c) rccl().comm_destroy(c);
+        if (c) m->api->comm_destroy(c);
     for (int r = 0; r < m->n; ++r) {
         (void)hipSetDevice(m->dev[r]);
         if (m->tile[r]) (void)hipFree(m->tile[r]);
@@ -1977,7 +1569,7 @@ int rt_multi_render_device(rt_multi *m, const rt_camera *camera, const rt_params
     // 2. the gather: tile r -> slot r of the gather buffer on rank 0's device
     const size_t slot_bytes = static_cast<size_t>(rows_max) * row_vals * es;
     if (N > 1 && m->rccl) {
-        const rccl_api &api = rccl();
+        const rccl_api &api = *m->api;
         ncclResult_t nr = api.group_start();
         for (int r = 1; r < N && nr == ncclSuccess; ++r) {
             const size_t cnt = static_cast<size_t>(multi_rows(H, N, r)) * row_vals;
@@ -2135,18 +1727,5 @@ int rt_render_multi_rgb8(const rt_sphere *spheres, uint32_t n_spheres, const rt_
                              stats);
 }
 
-// app::save_to_file, src/main.cxx:87-101: "P6\n<width> <height>\n255\n", then the texels.
-int rt_write_ppm(const char *path, const uint8_t *rgb, uint32_t width, uint32_t height)
-{
-    if (!path || (!rgb && width && height)) return fail(RT_ERR_INVALID, "rt_write_ppm: null argument");
-    std::FILE *f = std::fopen(path, "wb");
-    if (!f) return fail(RT_ERR_IO, std::string("rt_write_ppm: bad file ") + path);
-    const std::string hdr = "P6\n" + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
-    const size_t n = static_cast<size_t>(width) * height * 3u;
-    const bool ok = std::fwrite(hdr.data(), 1, hdr.size(), f) == hdr.size() && (n == 0 || std::fwrite(rgb, 1, n, f) == n);
-    const bool closed = std::fclose(f) == 0;
-    if (!ok || !closed) return fail(RT_ERR_IO, std::string("rt_write_ppm: write failed: ") + path);
-    return RT_OK;
-}
 
 } // extern "C"

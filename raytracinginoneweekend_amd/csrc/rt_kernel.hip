@@ -955,46 +955,28 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 } else {
                 if (lane == 0) c = atomicAdd(P.queue_ctr + q * kQueueStride, 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
-                if (P.guided_l2b < 0.f) {
-                    // guided: queue q owns blocks [qb0, qb1) of 64 items; ticket c takes blocks
-                    // [S(c), S(c+1)), S(t) = min(B, floor(B (1 - beta^t)) + 2t): chunks shrink
-                    // geometrically from ~B / (K waves per queue) to 2 blocks, so a queue is
-                    // served by few atomics and its last chunks are small. S is the same
-                    // function for every wave, so consecutive tickets tile the range; the 2t
-                    // term keeps it increasing even if exp2 or the float product is off by an
-                    // ulp (one block at most).
-                    const uint32_t qb0 = (uint32_t)(((uint64_t)P.n_blocks * q) >> 3);
-                    const uint32_t B = (uint32_t)(((uint64_t)P.n_blocks * (q + 1u)) >> 3) - qb0;
-                    auto S = [&](uint32_t t) -> uint32_t {
-                        const float x = t ? exp2f((float)t * P.guided_l2b) : 1.f;
-                        const uint64_t g = (uint64_t)floorf((float)B * (1.f - x)) + 2ull * t;
-                        return g < B ? (uint32_t)g : B;
-                    };
-                    const uint32_t s0 = __builtin_amdgcn_readfirstlane(S(c));
-                    if (s0 >= B) {
-                        q = (q + 1u) & 7u;
-                        if (++q_tried == 8u) exhausted = true;
-                        continue;
-                    }
-                    cnext = 64u * (qb0 + s0);
-                    cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), P.n_items));
-                } else {
-                const uint64_t chunk = (uint64_t)q + 8ull * c;
-                if (chunk >= P.n_chunks) {
+                // guided: queue q owns blocks [qb0, qb1) of 64 items; ticket c takes blocks
+                // [S(c), S(c+1)), S(t) = min(B, floor(B (1 - beta^t)) + 2t): chunks shrink
+                // geometrically from ~B / (K waves per queue) to 2 blocks, so a queue is
+                // served by few atomics and its last chunks are small. S is the same
+                // function for every wave, so consecutive tickets tile the range; the 2t
+                // term keeps it increasing even if exp2 or the float product is off by an
+                // ulp (one block at most).
+                const uint32_t qb0 = (uint32_t)(((uint64_t)P.n_blocks * q) >> 3);
+                const uint32_t B = (uint32_t)(((uint64_t)P.n_blocks * (q + 1u)) >> 3) - qb0;
+                auto S = [&](uint32_t t) -> uint32_t {
+                    const float x = t ? exp2f((float)t * P.guided_l2b) : 1.f;
+                    const uint64_t g = (uint64_t)floorf((float)B * (1.f - x)) + 2ull * t;
+                    return g < B ? (uint32_t)g : B;
+                };
+                const uint32_t s0 = __builtin_amdgcn_readfirstlane(S(c));
+                if (s0 >= B) {
                     q = (q + 1u) & 7u;
                     if (++q_tried == 8u) exhausted = true;
                     continue;
                 }
-                // big chunks first, then 64-item chunks for the end of the launch: a wave
-                // then holds at most 64 undealt items when the queues run dry
-                if (chunk < P.n_big_chunks) {
-                    cnext = (uint32_t)chunk * P.chunk_items;
-                    cend = cnext + P.chunk_items;
-                } else {
-                    cnext = P.n_big_chunks * P.chunk_items + ((uint32_t)chunk - P.n_big_chunks) * 64u;
-                    cend = min(cnext + 64u, P.n_items);
-                }
-                }
+                cnext = 64u * (qb0 + s0);
+                cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), P.n_items));
                 }
             }
             const uint32_t avail = cend - cnext;
@@ -1947,6 +1929,17 @@ hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t ld
     const void *fn = render_ptr(variant, cull, false);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
+}
+
+// the static LDS of a render kernel (per-wave and per-lane arrays; the scene blob comes on top)
+hipError_t static_lds_render(int variant, int cull, size_t *bytes)
+{
+    const void *fn = render_ptr(variant, cull, false);
+    if (!fn) return hipErrorInvalidValue;
+    hipFuncAttributes a{};
+    const hipError_t e = hipFuncGetAttributes(&a, fn);
+    if (e == hipSuccess) *bytes = a.sharedSizeBytes;
+    return e;
 }
 
 hipError_t launch_wave_gen(const KWave &w, hipStream_t stream)

@@ -6,6 +6,7 @@ DeviceScene.render         async on a caller stream into a device buffer (rt_ren
 MultiContext               row tiles over ranks (devices), gathered to rank 0 (rt_multi_*)
 save_ppm                   app::save_to_file (src/main.cxx:87-101), rt_write_ppm
 """
+import contextlib
 import ctypes as C
 import os
 
@@ -23,6 +24,55 @@ def make_params(width, height, spp, max_depth=64, seed=1234, row_offset=0, row_s
         | (abi.RT_FLAG_FAST_MATH if fast_math else 0) | (abi.RT_FLAG_BRUTE_FORCE if brute_force else 0) \
         | (abi.RT_FLAG_CUDA_COMPAT if cuda_compat else 0) | (abi.RT_FLAG_WAVEFRONT if wavefront else 0)
     return abi.RtParams(width, height, spp, max_depth, seed, row_offset, row_stride, num_rows, flags)
+
+
+def options(base=None, **fields):
+    """An rt_options record: the library defaults (or `base`) with `fields` set; diag bits by name
+    (ieee_roots=True, stats=True, ...; include/rt_api.h rt_diag) or as diag=<int>."""
+    o = abi.RtOptions()
+    if base is None:
+        check(lib().rt_options_default(C.byref(o)))
+    else:
+        C.memmove(C.byref(o), C.byref(base), C.sizeof(o))
+    for k, v in fields.items():
+        if k in abi.RT_DIAG:
+            o.diag = (o.diag | abi.RT_DIAG[k]) if v else (o.diag & ~abi.RT_DIAG[k])
+        elif k in dict(abi.RtOptions._fields_) and k != "size":
+            setattr(o, k, int(v))
+        else:
+            raise KeyError(f"rt_options has no field {k!r}")
+    return o
+
+
+def parse_options(text, base=None):
+    """rt_options_parse: "key=value,..." over `base` (default: the library defaults)."""
+    o = options(base)
+    check(lib().rt_options_parse(text.encode(), C.byref(o)))
+    return o
+
+
+def default_options():
+    """The process default (rt_get_default_options): library defaults with RT_OPTIONS applied."""
+    o = abi.RtOptions()
+    check(lib().rt_get_default_options(C.byref(o)))
+    return o
+
+
+def set_default_options(opt=None):
+    """rt_set_default_options (None: the library defaults)."""
+    check(lib().rt_set_default_options(C.byref(opt) if opt is not None else None))
+
+
+@contextlib.contextmanager
+def default_options_set(**fields):
+    """Within the block, scenes created without explicit options (the synchronous renders,
+    DeviceScene(), MultiContext()) use the current defaults with `fields` changed."""
+    prev = default_options()
+    set_default_options(options(prev, **fields))
+    try:
+        yield
+    finally:
+        set_default_options(prev)
 
 
 def _scene_arrays(scene):
@@ -92,15 +142,16 @@ class MultiContext:
     on devices[r]; tiles are gathered to rank 0 (RCCL when every rank has its own device,
     device copies for ranks sharing rank 0's device) and de-interleaved into the frame."""
 
-    def __init__(self, scene, devices=None, n_ranks=0):
+    def __init__(self, scene, devices=None, n_ranks=0, options=None):
         s, m = _scene_arrays(scene)
         h = C.c_void_p()
         devs = None
         if devices is not None:
             devs = (C.c_int * len(devices))(*devices)
             n_ranks = len(devices)
-        check(lib().rt_multi_create(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
-                                    abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), devs, n_ranks, C.byref(h)))
+        check(lib().rt_multi_create_ex(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
+                                       abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), devs, n_ranks,
+                                       C.byref(options) if options is not None else None, C.byref(h)))
         self.handle = h
         n, r = C.c_int(0), C.c_int(0)
         check(lib().rt_multi_info(h, C.byref(n), C.byref(r)))
@@ -149,12 +200,13 @@ def render_cuda_impl(width, height):
 class DeviceScene:
     """A scene resident in HBM on one device (rt_scene_create); renders are stream-ordered."""
 
-    def __init__(self, scene, device=0):
+    def __init__(self, scene, device=0, options=None):
         s, m = _scene_arrays(scene)
         self.n_spheres, self.n_materials = len(s), len(m)
         h = C.c_void_p()
-        check(lib().rt_scene_create(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
-                                    abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), device, C.byref(h)))
+        check(lib().rt_scene_create_ex(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
+                                       abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), device,
+                                       C.byref(options) if options is not None else None, C.byref(h)))
         self.handle = h
         self.device = device
 
@@ -165,6 +217,12 @@ class DeviceScene:
                                      C.c_void_p(d_rgb), C.c_void_p(stream or 0),
                                      C.c_void_p(d_segments) if d_segments else None))
 
+    def usage(self):
+        """rt_scene_usage_get: device bytes held and the last render's cut, as a dict."""
+        u = abi.RtSceneUsage()
+        check(lib().rt_scene_usage_get(self.handle, C.byref(u)))
+        return {k: getattr(u, k) for k, _ in abi.RtSceneUsage._fields_ if k != "reserved"}
+
     def kernel_times(self, max_calls=256):
         """Render-kernel durations (ms) of the most recent render() calls, oldest first."""
         buf = (C.c_float * max_calls)()
@@ -173,7 +231,7 @@ class DeviceScene:
         return list(buf[:n.value])
 
     def debug_counters(self, reset=True):
-        """Counters of the instrumented kernel (RT_DEBUG_STATS=1), see rt_scene_debug_counters."""
+        """Counters of the instrumented kernel (options stats=True), see rt_scene_debug_counters."""
         buf = (C.c_uint64 * 16)()
         check(lib().rt_scene_debug_counters(self.handle, buf, 1 if reset else 0))
         keys = ["wave_iters", "wave_refills", "wave_blocks", "lane_blocks", "wave_roots", "lane_roots", "segments",
@@ -188,14 +246,14 @@ class DeviceScene:
               "iso_lanes", "walk_skipped"]
 
     def debug_events(self, reset=True):
-        """Block-execution counts of the instrumented kernel (RT_DEBUG_STATS=1), see rt_scene_debug_events."""
+        """Block-execution counts of the instrumented kernel (options stats=True), see rt_scene_debug_events."""
         buf = (C.c_uint64 * 32)()
         check(lib().rt_scene_debug_events(self.handle, buf, 1 if reset else 0))
         return dict(zip(self.EVENTS, list(buf)))
 
     def debug_timeline(self, max_waves=65536):
         """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry) of the last
-        instrumented launch (RT_DEBUG_STATS=1; dry = when the wave found every queue empty; times
+        instrumented launch (options stats=True; dry = when the wave found every queue empty; times
         in ticks of the 100 MHz clock), see rt_scene_debug_timeline."""
         buf = (C.c_uint64 * (4 * max_waves))()
         n = C.c_uint32(0)

@@ -2,7 +2,10 @@
 """A/B the render-kernel variants in ONE process, interleaved rounds (guide §5.4 rule 24).
 
 Every variant must produce bit-identical frames; prints per-variant median/min kernel ms.
-    python scripts/ab_variants.py [--config c3] [--rounds 5] [--variants lds:4,scalar:4,...]
+    python scripts/ab_variants.py [--config c3] [--rounds 5] [--variants exact:cull,exact:cull:transpose_max=0,...]
+A variant is kind:traversal[:options][:s0]: kind exact|fast|scalar, traversal cull|brute,
+options in rt_options_parse syntax with ';' between fields (each variant gets its own scene
+with them, over the process default), s0: no segment counters. --stats: the instrumented kernel.
 """
 import argparse
 import json
@@ -23,28 +26,29 @@ ap.add_argument("--camera", default="reference")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--depth", type=int, default=0, help="override the config's max depth")
 ap.add_argument("--variants", default="exact:cull,exact:brute,fast:cull,fast:brute")
+ap.add_argument("--stats", action="store_true", help="the instrumented kernel (counters and per-wave timeline)")
+ap.add_argument("--timeline-out", default="", help="with --stats: dump raw per-wave records to <prefix>.<variant>.json")
 a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
 depth = a.depth or depth
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H, rt.CORRECTED if a.camera == "corrected" else rt.REFERENCE)
-ds = rt.DeviceScene(arrays)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
-# kind:traversal[:cN][:LN][:tN] -- "cN" RT_CHUNK_ITEMS=N, "L0"/"L1" RT_SHADE_LDS, "tN" RT_TAIL_PCT=N,
-# "r0"/"r1" RT_ROOT_BOX, "s0" no counters, "xN" RT_TRANSPOSE_MAX=N
 variants = [(v.split(":")[0], v.split(":")[1], v.split(":")[2:]) for v in a.variants.split(",")]
 times = {":".join([k, t] + x): [] for k, t, x in variants}
+scenes = {}
+for kind, trav, extra in variants:
+    o = rt.parse_options(";".join(x for x in extra if x != "s0"), rt.default_options())
+    if a.stats:
+        o = rt.options(o, stats=True)
+    scenes[":".join([kind, trav] + extra)] = rt.DeviceScene(arrays, options=o)
 ref = None
 segs = {}
 for r in range(a.rounds + 1):
     for kind, trav, extra in variants:
-        os.environ["RT_CHUNK_ITEMS"] = "".join(x[1:] for x in extra if x.startswith("c"))
-        os.environ["RT_SHADE_LDS"] = "".join(x[1:] for x in extra if x.startswith("L"))
-        os.environ["RT_TAIL_PCT"] = "".join(x[1:] for x in extra if x.startswith("t"))
-        os.environ["RT_ROOT_BOX"] = "".join(x[1:] for x in extra if x.startswith("r"))
-        os.environ["RT_TRANSPOSE_MAX"] = "".join(x[1:] for x in extra if x.startswith("x"))
+        ds = scenes[":".join([kind, trav] + extra)]
         p = rt.make_params(W, H, spp, depth, 1234, scalar_scene=kind == "scalar", fast_math=kind == "fast",
                            brute_force=trav == "brute")
         seg.zero_()
@@ -64,7 +68,7 @@ for r in range(a.rounds + 1):
             print(f"{name}: identical={same} segments={segs[name]} max|d|={d.max().item():.3g} "
                   f"mean|d|={d.mean().item():.3g} px<=1e-4: {(px <= 1e-4).float().mean().item()*100:.3f}% "
                   f"px<=1e-3: {(px <= 1e-3).float().mean().item()*100:.3f}%", flush=True)
-            if os.environ.get("RT_DEBUG_STATS") == "1":
+            if a.stats:
                 cnt = ds.debug_counters()
                 print(f"{name}: counters {cnt}", flush=True)
                 tl = [r for r in ds.debug_timeline() if r[1] >= r[0] > 0]
@@ -84,7 +88,7 @@ for r in range(a.rounds + 1):
                           f"  iterations   {qs([r[2] for r in tl], 1, 0)}\n"
                           f"  iters after dry {qs([r[5] for r in tl], 1, 0)}\n"
                           f"  refills      {qs([r[4] for r in tl], 1, 0)}", flush=True)
-                    dump = os.environ.get("RT_TIMELINE_OUT")
+                    dump = a.timeline_out
                     if dump:  # raw per-wave records for offline analysis
                         with open(f"{dump}.{name.replace(':', '_')}.json", "w") as fh:
                             json.dump(ds.debug_timeline(), fh)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Wave-level efficiency counters of the instrumented render kernel (RT_DEBUG_STATS=1) on a
+"""Wave-level efficiency counters of the instrumented render kernel (rt_options stats=1) on a
 bench config: live lanes per wave iteration, lane occupancy of the member-sphere blocks and of
 the root work, cycles per loop region.   python scripts/stats_c3.py [--config c3]
 """
@@ -10,7 +10,6 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-os.environ["RT_DEBUG_STATS"] = "1"
 import torch  # noqa: E402
 
 import raytracinginoneweekend_amd as rt  # noqa: E402
@@ -23,7 +22,7 @@ a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H, rt.CORRECTED if a.camera == "corrected" else rt.REFERENCE)
-ds = rt.DeviceScene(arrays)
+ds = rt.DeviceScene(arrays, options=rt.options(rt.default_options(), stats=True))
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 seg = torch.zeros(3, dtype=torch.int64, device="cuda")
 p = rt.make_params(W, H, spp, depth, 1234)

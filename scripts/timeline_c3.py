@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Where a lone frame's render launch spends its time (RT_DEBUG_STATS=1 build of the render
+"""Where a lone frame's render launch spends its time (rt_options stats=1 build of the render
 kernel): per-wave times at which the wave found every item queue dry and at which it exited,
 relative to the earliest wave start, plus the same frame's uninstrumented single-launch time.
     python scripts/timeline_c3.py [--config c3] [--camera reference] [--rehearse-world N]
@@ -11,7 +11,6 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-os.environ["RT_DEBUG_STATS"] = "1"
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -26,7 +25,7 @@ a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H, rt.CORRECTED if a.camera == "corrected" else rt.REFERENCE)
-ds = rt.DeviceScene(arrays)
+ds = rt.DeviceScene(arrays, options=rt.options(rt.default_options(), stats=True))
 N = a.rehearse_world
 rows = (H + N - 1) // N
 out = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")

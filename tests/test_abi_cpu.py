@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version():
-    assert rt.lib().rt_version() == 1
+    assert rt.lib().rt_version() == 2
 
 
 def test_huge_scene_generator_matches_reference():
@@ -187,3 +187,76 @@ def test_timed_kernel_code_hash():
     h = bench.kernel_sha256()
     assert h is not None and len(h) == 64
     assert bench.kernel_sha256("no_such_kernel") is None
+
+
+# ---- rt_options: the library's only tuning surface besides GPU_MAX_HW_QUEUES and RT_OPTIONS ----
+def test_options_defaults_and_parse():
+    o = rt.options()
+    assert o.size == C.sizeof(abi.RtOptions)
+    assert (o.render_streams, o.workspaces_per_stream, o.deep_split, o.max_pass_bytes, o.max_workspace_bytes,
+            o.deep_min_items, o.cluster_size, o.transpose_max, o.wave_queue_rays, o.diag) == \
+        (0, 2, 8, 2 << 30, 0, 1 << 25, 16, 16, 1 << 25, 0)
+    p = rt.parse_options("render_streams=3, max_workspace_bytes=0x100000000;deep_split=0 ieee_roots=1,stats=1")
+    assert (p.render_streams, p.max_workspace_bytes, p.deep_split) == (3, 1 << 32, 0)
+    assert p.diag == abi.RT_DIAG["ieee_roots"] | abi.RT_DIAG["stats"]
+    assert rt.parse_options("stats=0", p).diag == abi.RT_DIAG["ieee_roots"]
+    assert rt.parse_options("").render_streams == 0  # empty text: unchanged
+
+
+@pytest.mark.parametrize("text,field", [
+    ("render_streams=9", "render_streams"), ("workspaces_per_stream=0", "workspaces_per_stream"),
+    ("workspaces_per_stream=3", "workspaces_per_stream"), ("deep_split=2000", "deep_split"),
+    ("max_pass_bytes=0", "max_pass_bytes"), ("max_pass_bytes=4294967296", "max_pass_bytes"),
+    ("cluster_size=6", "cluster_size"), ("cluster_size=68", "cluster_size"), ("transpose_max=17", "transpose_max"),
+    ("wave_queue_rays=10", "wave_queue_rays"), ("diag=4096", "diag"), ("shade_lds=1,shade_global=1", "diag"),
+    ("bogus=1", "bogus"), ("render_streams", "key=value"), ("render_streams=-1", "render_streams"),
+    ("render_streams=x", "render_streams"), ("stats=2", "stats"), ("deep_split=4294967296", "deep_split")])
+def test_options_rejected_with_the_field_named(text, field):
+    base = rt.options()
+    with pytest.raises(rt.RtError) as e:
+        rt.parse_options(text, base)
+    assert e.value.status == abi.RT_ERR_INVALID and field in str(e.value)
+    assert base.render_streams == 0 and base.diag == 0  # the record is left as it was
+
+
+def test_default_options_set_and_restore():
+    before = rt.default_options()
+    with rt.default_options_set(render_streams=5, no_shortcut=True):
+        d = rt.default_options()
+        assert d.render_streams == 5 and d.diag & abi.RT_DIAG["no_shortcut"]
+    after = rt.default_options()
+    assert bytes(after) == bytes(before)
+    bad = rt.options()
+    bad.size = 12
+    with pytest.raises(rt.RtError) as e:
+        rt.set_default_options(bad)
+    assert "size" in str(e.value)
+
+
+def test_rt_options_environment_applies_and_fails_loudly():
+    """RT_OPTIONS is parsed once over the defaults; a malformed value makes every scene created
+    without explicit options fail with the parser's message (never a silent default)."""
+    import subprocess
+    import sys
+    code = ("import raytracinginoneweekend_amd as rt; o = rt.default_options(); "
+            "print(o.render_streams, o.deep_split, o.max_workspace_bytes, o.diag)")
+    env = dict(os.environ, RT_OPTIONS="render_streams=4,deep_split=0,max_workspace_bytes=4294967296,no_root_box=1")
+    out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["4", "0", "4294967296", str(abi.RT_DIAG["no_root_box"])]
+    env["RT_OPTIONS"] = "render_streams=40"
+    out = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True)
+    assert out.returncode != 0 and "RT_OPTIONS" in out.stderr and "render_streams" in out.stderr
+
+
+def test_multi_create_rejects_mixed_device_lists_before_any_device_call():
+    """rt_multi_create accepts device lists that are all distinct (RCCL) or all rank 0's device
+    (virtual ranks); a mix is RT_ERR_INVALID, decided before any HIP call (so also here, without a
+    GPU), and the stand-in transport needs virtual ranks."""
+    s, m = rt.simple_scene_arrays()
+    for devs in ([0, 0, 1], [0, 1, 0], [1, 1, 2, 3]):
+        with pytest.raises(rt.RtError) as e:
+            rt.MultiContext((s, m), devices=devs)
+        assert e.value.status == abi.RT_ERR_INVALID and "distinct" in str(e.value)
+    with pytest.raises(rt.RtError) as e:
+        rt.MultiContext((s, m), devices=[0, 1], options=rt.options(standin_transport=True))
+    assert e.value.status == abi.RT_ERR_INVALID and "stand-in" in str(e.value)

@@ -98,11 +98,9 @@ def test_full_config_frame_matches_reference_rows(cfg):
     s, m = G.scene("huge")
     img, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 1234, full_frame=True))
     assert st.primaries == W * H * spp
-    # the whole frame against the reference's own full render, when its digest is committed
-    try:
-        _assert_frame_digest(img, _full_ref(cfg), cfg)
-    except KeyError:
-        pass
+    # the whole frame against the reference's own full render (its digest must be committed:
+    # tests/golden/make_fullframe.py; a missing digest fails)
+    _assert_frame_digest(img, _full_ref(cfg), cfg)
     # the reference's own row (tests/golden/make_golden.py, oracle/_ref)
     meta, f32, u8 = G.render(c["golden"])
     y = meta["row_offset"]
@@ -202,16 +200,16 @@ def test_ppm_of_gpu_frame_matches_reference_ppm(tmp_path):
 
 
 # ---- caller streams that change between calls -----------------------------------
-@pytest.mark.parametrize("pipeline,budget_samples", [("", 4), ("0", 4), ("0", 0), ("3", 0)])
-def test_alternating_caller_streams(pipeline, budget_samples, monkeypatch):
+@pytest.mark.parametrize("streams,budget_samples", [(0, 4), (1, 4), (1, 0), (3, 0)])
+def test_alternating_caller_streams(streams, budget_samples, opts):
     """One scene, renders alternating between two caller streams without host sync: the
-    shared accumulation buffer (multi-pass frames), the workspaces (RT_PIPELINE=0) and the
+    shared accumulation buffer (multi-pass frames), the workspaces (render_streams = 1) and the
     counters must never be used by both streams at once. Every frame equals its oracle."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("RT_PIPELINE", pipeline)
+    opts.set(render_streams=streams)
     W, H = 48, 32
     if budget_samples:
-        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_samples))
+        opts.set(max_pass_bytes=W * H * 12 * budget_samples)
     s, m = G.scene("huge")
     ds = rt.DeviceScene((s, m))
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
@@ -232,14 +230,14 @@ def test_alternating_caller_streams(pipeline, budget_samples, monkeypatch):
 
 
 # ---- the wavefront variant (RT_FLAG_WAVEFRONT) -------------------------------
-@pytest.mark.parametrize("queue_rays", ["", "1000"])
-def test_wavefront_variant_matches_megakernel(queue_rays, monkeypatch):
+@pytest.mark.parametrize("queue_rays", [0, 1000])
+def test_wavefront_variant_matches_megakernel(queue_rays, opts):
     """Per-segment launches through HBM ray queues (wave_gen_kernel, wave_bounce_kernel): the
     same frames, bit for bit, and the same segment counts as the persistent megakernel, on the
     huge scene (culled walk) and the simple scene (brute force, shading records in LDS), for
-    depth limits 0..64, both cameras, and chunks smaller than a pass (RT_WAVE_QUEUE_RAYS)."""
+    depth limits 0..64, both cameras, and chunks smaller than a pass (wave_queue_rays)."""
     if queue_rays:
-        monkeypatch.setenv("RT_WAVE_QUEUE_RAYS", queue_rays)
+        opts.set(wave_queue_rays=queue_rays)
     for scene in ("huge", "simple"):
         s, m = G.scene(scene)
         for (W, H, spp, depth, mode) in [(64, 36, 4, 64, 0), (48, 27, 3, 64, 1), (40, 20, 5, 1, 0), (32, 16, 2, 0, 0),
@@ -251,7 +249,7 @@ def test_wavefront_variant_matches_megakernel(queue_rays, monkeypatch):
             assert sb.segments == sa.segments and sb.primaries == sa.primaries
 
 
-def test_wavefront_variant_golden_and_multipass(monkeypatch):
+def test_wavefront_variant_golden_and_multipass(opts):
     """The wavefront variant against the reference's own frame (golden huge_64x36_s4) and a
     multi-pass render (slot budget of 8 samples) against the oracle."""
     meta, f32, _ = G.render("huge_64x36_s4")
@@ -260,8 +258,7 @@ def test_wavefront_variant_golden_and_multipass(monkeypatch):
     img, _ = rt.render_f32((s, m), p)
     _bits_equal(img, f32, "golden huge_64x36_s4")
     W, H, spp = 40, 24, 21
-    monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * 8))
-    monkeypatch.setenv("RT_WAVE_QUEUE_RAYS", "2000")
+    opts.set(max_pass_bytes=W * H * 12 * 8, wave_queue_rays=2000)
     cam = O.camera_default(W, H)
     img, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 3, wavefront=True), cam)
     want, want_seg = O.render_f32(s, m, cam, rt.make_params(W, H, spp, 64, 3))
@@ -270,44 +267,43 @@ def test_wavefront_variant_golden_and_multipass(monkeypatch):
 
 
 # ---- the deep-path split (RT_DEEP_SPLIT, render_kernel deep queue) --------------------------
-@pytest.mark.parametrize("split", ["1", "3", "8"])
-def test_deep_split_matches_unsplit(split, monkeypatch):
-    """Paths that have traced RT_DEEP_SPLIT segments move to the deep queue and finish in a second
+@pytest.mark.parametrize("split", [1, 3, 8])
+def test_deep_split_matches_unsplit(split, opts):
+    """Paths that have traced deep_split segments move to the deep queue and finish in a second
     launch: the same frames, bit for bit, and the same segment counts as without the split
-    (RT_DEEP_SPLIT=0), for both cameras, depth limits around the split, multi-pass frames (slot
+    (deep_split = 0), for both cameras, depth limits around the split, multi-pass frames (slot
     budget of 8 samples) and a deep queue that overflows (split 1 on 230 K samples with the
     corrected camera: 8 regions of 512 paths, most paths continue past their first segment),
     whose extra paths stay in the main launch. Configs 4 and 5 (test_full_config_frame_...) run
-    with the default split, their passes being above RT_DEEP_MIN_ITEMS."""
-    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")  # split passes of any size
+    with the default split, their passes being above deep_min_items."""
+    opts.set(deep_min_items=0)  # split passes of any size
     s, m = G.scene("huge")
-    cases = [(64, 36, 4, 64, 0, 0), (48, 27, 3, 64, 1, 0), (40, 20, 5, int(split), 0, 0),
-             (33, 17, 9, int(split) + 1, 1, 0), (40, 24, 21, 64, 0, 8), (160, 90, 16, 64, 1, 0)]
+    cases = [(64, 36, 4, 64, 0, 0), (48, 27, 3, 64, 1, 0), (40, 20, 5, split, 0, 0),
+             (33, 17, 9, split + 1, 1, 0), (40, 24, 21, 64, 0, 8), (160, 90, 16, 64, 1, 0)]
     for (W, H, spp, depth, mode, budget) in cases:
         cam = rt.Camera.default(W, H, mode)
         if budget:
-            monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget))
-        monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+            opts.set(max_pass_bytes=W * H * 12 * budget)
+        opts.set(deep_split=0)
         a, sa = rt.render_f32((s, m), rt.make_params(W, H, spp, depth, 11), cam)
-        monkeypatch.setenv("RT_DEEP_SPLIT", split)
+        opts.set(deep_split=split)
         b, sb = rt.render_f32((s, m), rt.make_params(W, H, spp, depth, 11), cam)
-        monkeypatch.delenv("RT_SLOT_BUDGET_BYTES", raising=False)
+        opts.clear("max_pass_bytes")
         _bits_equal(b, a, f"split {split}: {W}x{H} spp {spp} depth {depth} camera {mode}")
         assert sb.segments == sa.segments and sb.primaries == sa.primaries
 
 
-def test_deep_split_against_oracle_and_golden(monkeypatch):
+def test_deep_split_against_oracle_and_golden(opts):
     """With the split at 2 segments (most continuing paths go through the deep queue): the
     reference's own frame (golden huge_64x36_s4) and the oracle on a multi-pass render."""
-    monkeypatch.setenv("RT_DEEP_SPLIT", "2")
-    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
+    opts.set(deep_split=2, deep_min_items=0)
     meta, f32, _ = G.render("huge_64x36_s4")
     s, m = G.scene("huge")
     img, _ = rt.render_f32((s, m), rt.make_params(meta["width"], meta["height"], meta["spp"], meta["depth"],
                                                   meta["seed"]))
     _bits_equal(img, f32, "golden huge_64x36_s4")
     W, H, spp = 40, 24, 21
-    monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * 8))
+    opts.set(max_pass_bytes=W * H * 12 * 8)
     cam = O.camera_default(W, H, abi.RT_CAMERA_CORRECTED)
     img, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 5), rt.Camera.default(W, H, rt.CORRECTED))
     want, want_seg = O.render_f32(s, m, cam, rt.make_params(W, H, spp, 64, 5))
@@ -315,15 +311,14 @@ def test_deep_split_against_oracle_and_golden(monkeypatch):
     assert st.segments == want_seg
 
 
-def test_deep_split_overflow_feedback(monkeypatch):
+def test_deep_split_overflow_feedback(opts):
     """One scene, frames with two cameras streamed without host sync, split at 1 segment on every
     pass: the corrected camera's passes overflow the deep queue, report it through host memory,
     and its later frames run unsplit, while the reference camera's frames keep the split. Every
     frame equals the unsplit render, bit for bit, with the same segment count."""
     torch = pytest.importorskip("torch")
     import time
-    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
-    monkeypatch.setenv("RT_DEEP_SPLIT", "1")
+    opts.set(deep_min_items=0, deep_split=1)
     W, H, spp = 160, 90, 16
     s, m = G.scene("huge")
     cams = [rt.Camera.default(W, H, rt.CORRECTED), rt.Camera.default(W, H)]
@@ -340,7 +335,7 @@ def test_deep_split_overflow_feedback(monkeypatch):
             time.sleep(0.01)
     torch.cuda.synchronize()
     ds.close()
-    monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+    opts.set(deep_split=0)
     for c, cam in enumerate(cams):
         want, want_st = rt.render_f32((s, m), p, cam)
         for k in range(c, 8, 2):
@@ -349,14 +344,13 @@ def test_deep_split_overflow_feedback(monkeypatch):
 
 
 
-@pytest.mark.parametrize("pipeline", ["", "0"])
-def test_deep_split_variants_and_row_shares(pipeline, monkeypatch):
+@pytest.mark.parametrize("streams", [0, 1])
+def test_deep_split_variants_and_row_shares(streams, opts):
     """The split with the render variants (fast-math; brute force, the scalar-cache scene and the
     simple scene, which walk every sphere and are not split), on the caller's stream alone
-    (RT_PIPELINE=0) or on the render streams, and for interleaved row shares: each equals its
+    (render_streams = 1) or on the render streams, and for interleaved row shares: each equals its
     unsplit render."""
-    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
-    monkeypatch.setenv("RT_PIPELINE", pipeline)
+    opts.set(deep_min_items=0, render_streams=streams)
     W, H, spp = 72, 40, 8
     for scene, kw, rows in [("huge", dict(fast_math=True), {}), ("huge", dict(brute_force=True), {}),
                             ("huge", dict(scalar_scene=True), {}), ("simple", {}, {}),
@@ -364,22 +358,21 @@ def test_deep_split_variants_and_row_shares(pipeline, monkeypatch):
         s, m = G.scene(scene)
         cam = rt.Camera.default(W, H)
         p = rt.make_params(W, H, spp, 64, 9, **rows, **kw)
-        monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+        opts.set(deep_split=0)
         a, sa = rt.render_f32((s, m), p, cam)
-        monkeypatch.setenv("RT_DEEP_SPLIT", "2")
+        opts.set(deep_split=2)
         b, sb = rt.render_f32((s, m), p, cam)
         _bits_equal(b, a, f"{scene} {kw} {rows}")
         assert sb.segments == sa.segments
 
 
-def test_deep_split_streams_passes_of_changing_size(monkeypatch):
+def test_deep_split_streams_passes_of_changing_size(opts):
     """One DeviceScene, split passes of different pixel and sample counts streamed without host
     sync, so every workspace's deep-queue buffer serves passes of other sizes (its pixel flags
     must start cleared whatever the previous pass left there: rt_host.cpp deep_clean). Each
     frame equals its unsplit render, bit for bit, with the same segment count."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
-    monkeypatch.setenv("RT_DEEP_SPLIT", "2")
+    opts.set(deep_min_items=0, deep_split=2)
     s, m = G.scene("huge")
     sizes = [(160, 90, 16), (48, 27, 3), (200, 120, 8), (64, 36, 4), (96, 54, 12), (40, 20, 5)] * 3
     ds = rt.DeviceScene((s, m))
@@ -392,8 +385,128 @@ def test_deep_split_streams_passes_of_changing_size(monkeypatch):
                   stream, segs[-1].data_ptr())
     torch.cuda.synchronize()
     ds.close()
-    monkeypatch.setenv("RT_DEEP_SPLIT", "0")
+    opts.set(deep_split=0)
     for k, (W, H, spp) in enumerate(sizes):
         want, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 30 + k), rt.Camera.default(W, H, k % 2))
         _bits_equal(outs[k].cpu().numpy(), want, f"frame {k} {W}x{H}@{spp}")
         assert int(segs[k][0]) == st.segments
+
+
+# ---- the RCCL gather branch on one GPU (RT_DIAG_STANDIN_TRANSPORT) -------------------------
+@pytest.mark.parametrize("n", [2, 8])
+def test_multi_context_rccl_branch_with_standin_transport(n):
+    """rt_multi_render_device's RCCL branch — grouped send/recv per peer on the ranks' own
+    streams into slots of rank 0's gather buffer, then the de-interleave — with RCCL replaced by
+    stream-ordered device copies between virtual ranks (the stand-in keeps RCCL's stream
+    semantics: the receive waits for the sender's prior work, the sender's later work waits for
+    the copy). Frames of different sizes (ragged tiles), formats, cameras and spp, enqueued back
+    to back without host sync so that tiles and slots are reused while earlier frames are in
+    flight, each equal to its single-device render; then the synchronous entry points."""
+    torch = pytest.importorskip("torch")
+    s, m = G.scene("huge")
+    ctx = rt.MultiContext((s, m), devices=[0] * n, options=rt.options(standin_transport=True))
+    assert ctx.n_ranks == n and ctx.uses_rccl
+    jobs = [(48, 30, 8, 1, 0, False), (48, 30, 5, 2, 1, True), (64, 37, 12, 3, 0, False), (40, 9, 4, 4, 1, True),
+            (48, 30, 6, 5, 0, True), (64, 37, 3, 6, 1, False)] * 2
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for W, H, spp, seed, mode, u8 in jobs:
+        outs.append(torch.empty((H, W, 3), dtype=torch.uint8 if u8 else torch.float32, device="cuda"))
+        ctx.render_device(rt.Camera.default(W, H, mode), rt.make_params(W, H, spp, 64, seed), outs[-1].data_ptr(),
+                          stream, rgb8=u8)
+    torch.cuda.synchronize()
+    for (W, H, spp, seed, mode, u8), o in zip(jobs, outs):
+        p, cam = rt.make_params(W, H, spp, 64, seed), rt.Camera.default(W, H, mode)
+        if u8:
+            want, _ = rt.render_rgb8((s, m), p, cam)
+            np.testing.assert_array_equal(o.cpu().numpy(), want)
+        else:
+            want, _ = rt.render_f32((s, m), p, cam)
+            _bits_equal(o.cpu().numpy(), want, f"n={n} {W}x{H}@{spp}")
+    p = rt.make_params(64, 37, 4, 64, 5)
+    got, stm = ctx.render_f32(p)
+    single, st1 = rt.render_f32((s, m), p)
+    _bits_equal(got, single, "synchronous")
+    assert stm.segments == st1.segments
+    ctx.close()
+
+
+# ---- a bounded HBM footprint (rt_options.max_workspace_bytes) ------------------------------
+def test_workspace_cap_bounds_memory_with_the_same_bits(opts):
+    """Under max_workspace_bytes the library cuts a frame into smaller passes, then fewer
+    workspaces per stream, then fewer streams: the scene's workspaces stay within the cap
+    (rt_scene_usage_get), frames streamed without host sync keep the uncapped bits and segment
+    counts, and a cap below one 4-sample pass is RT_ERR_CAPACITY."""
+    torch = pytest.importorskip("torch")
+    s, m = G.scene("huge")
+    W, H, spp = 160, 90, 64
+    cam = rt.Camera.default(W, H)
+    p = rt.make_params(W, H, spp, 64, 17)
+    want, want_st = rt.render_f32((s, m), p, cam)
+    stream = torch.cuda.current_stream().cuda_stream
+    per_sample = W * H * 12
+    seen = set()
+    for cap in (0, 64 << 20, 8 << 20, 4 << 20, 1 << 20):
+        ds = rt.DeviceScene((s, m), options=rt.options(render_streams=7, max_workspace_bytes=cap))
+        outs, segs = [], []
+        for _ in range(4):
+            outs.append(torch.empty((H, W, 3), dtype=torch.float32, device="cuda"))
+            segs.append(torch.zeros(3, dtype=torch.int64, device="cuda"))
+            ds.render(cam, p, outs[-1].data_ptr(), stream, segs[-1].data_ptr())
+        torch.cuda.synchronize()
+        u = ds.usage()
+        ds.close()
+        for o, g in zip(outs, segs):
+            _bits_equal(o.cpu().numpy(), want, f"cap {cap}")
+            assert int(g[0]) == want_st.segments
+        if cap:
+            assert u["workspace_bytes"] <= cap, (cap, u)
+        assert u["workspace_bytes"] >= u["workspaces"] * u["pass_samples"] * per_sample
+        seen.add((u["render_streams"], u["workspaces"], u["pass_samples"]))
+    assert len(seen) >= 3  # the caps changed the cut
+    ds = rt.DeviceScene((s, m), options=rt.options(max_workspace_bytes=100 << 10))
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    with pytest.raises(rt.RtError) as e:
+        ds.render(cam, p, out.data_ptr(), stream)
+    assert e.value.status == abi.RT_ERR_CAPACITY
+    ds.close()
+
+
+# ---- scenes at the LDS limit (the kernel's static LDS counts, ADVICE r3) --------------------
+def test_scene_at_the_lds_limit_renders_or_is_refused():
+    """A scene whose blob fits the device's LDS per workgroup only without the render kernel's
+    static LDS (per-wave and per-lane arrays) must not reach a failing launch: brute force falls
+    back to the scalar-cache kernel (the oracle's bits), the culled walk is refused with
+    RT_ERR_UNSUPPORTED or renders correctly."""
+    probe = rt.DeviceScene(G.scene("simple"))
+    u = probe.usage()
+    probe.close()
+    assert 4096 < u["static_lds_bytes"] < 32768 and u["max_lds_bytes"] >= 65536
+    # the brute-force blob is 20 B per geo slot (n_geo = pad4(n) + 4) + 32 B before the shading
+    n_geo = ((u["max_lds_bytes"] - u["static_lds_bytes"] // 2 - 32) // 20) & ~3
+    n = n_geo - 4
+    rng = np.random.default_rng(3)
+    s = np.zeros(n, dtype=abi.SPHERE_DTYPE)
+    m = np.zeros(2, dtype=abi.MATERIAL_DTYPE)
+    m[0] = (0, [0.5, 0.5, 0.5], 0.0)
+    m[1] = (1, [0.7, 0.6, 0.5], 0.2)
+    s["center"][:, 0] = rng.uniform(-30, 30, n)
+    s["center"][:, 2] = rng.uniform(-30, 30, n)
+    s["center"][:, 1] = 0.1
+    s["radius"] = 0.1
+    s["material"] = rng.integers(0, 2, n)
+    s["center"][0], s["radius"][0] = (0, -1000, 0), 1000.0
+    assert 20 * n_geo + 32 <= u["max_lds_bytes"] < 20 * n_geo + 32 + u["static_lds_bytes"]
+    W, H, spp = 16, 8, 2
+    cam = O.camera_default(W, H, abi.RT_CAMERA_CORRECTED)
+    p = rt.make_params(W, H, spp, 8, 4)
+    want, seg = O.render_f32(s, m, cam, p)
+    got, st = rt.render_f32((s, m), rt.make_params(W, H, spp, 8, 4, brute_force=True), cam)
+    _bits_equal(got, want, "brute force at the LDS limit")
+    assert st.segments == seg
+    try:
+        got, st = rt.render_f32((s, m), p, cam)
+    except rt.RtError as e:
+        assert e.status == abi.RT_ERR_UNSUPPORTED, e
+    else:
+        _bits_equal(got, want, "culled at the LDS limit")

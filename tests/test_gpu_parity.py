@@ -18,11 +18,11 @@ pytestmark = pytest.mark.gpu
 
 RENDERS = sorted(n for n, m in G.manifest()["renders"].items() if m["rng"] == "pcg")
 # clustered0: the same two-level walk with every cluster's members tested per lane (never
-# transposed, RT_TRANSPOSE_MAX=0)
+# transposed, rt_options.transpose_max = 0)
 # ieee_roots: the IEEE sqrt/division sequences for the roots instead of their short exact forms
-# (RT_FAST_ROOTS=0; rt_kernel.hip RayDiv)
-VARIANTS = {"clustered": {}, "clustered0": {"_transpose": "0"}, "brute": {"brute_force": True},
-            "scalar": {"scalar_scene": True}, "ieee_roots": {"_env": ("RT_FAST_ROOTS", "0")}}
+# (RT_DIAG_IEEE_ROOTS; rt_kernel.hip RayDiv)
+VARIANTS = {"clustered": {}, "clustered0": {"_opts": {"transpose_max": 0}}, "brute": {"brute_force": True},
+            "scalar": {"scalar_scene": True}, "ieee_roots": {"_opts": {"ieee_roots": True}}}
 
 
 def _params(meta, **kw):
@@ -48,15 +48,12 @@ def _device():
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("name", RENDERS)
-def test_golden_render_f32(name, variant, monkeypatch):
+def test_golden_render_f32(name, variant, opts):
     meta, f32, _ = G.render(name)
     scene = G.scene(meta["scene"])
     cam = rt.Camera.default(meta["width"], meta["height"], G.camera_mode(meta))
     kw = dict(VARIANTS[variant])
-    if "_transpose" in kw:
-        monkeypatch.setenv("RT_TRANSPOSE_MAX", kw.pop("_transpose"))
-    if "_env" in kw:
-        monkeypatch.setenv(*kw.pop("_env"))
+    opts.set(**kw.pop("_opts", {}))
     img, st = rt.render_f32(scene, _params(meta, **kw), cam)
     _bits_equal(img, f32)
     assert st.primaries == meta["width"] * meta["num_rows"] * meta["spp"]
@@ -107,18 +104,18 @@ def test_empty_scene_is_sky():
     assert st.segments == st.primaries  # every primary misses
 
 
-@pytest.mark.parametrize("tile_lw", ["", "3", "4", "5", "6"])
-@pytest.mark.parametrize("W", [96, 128])
-def test_row_partition_invariance_full_frame(tile_lw, W, monkeypatch):
-    """Rows rendered by interleaved 'ranks' and stitched == one full render, bitwise, whatever
-    the tile shape (RT_TILE_LW; default 8x8; 64x1 falls back to 32x2 at W = 96)."""
+@pytest.mark.parametrize("W", [96, 128, 100])
+def test_row_partition_invariance_full_frame(W):
+    """Rows rendered by interleaved 'ranks' and stitched == one full render, bitwise, for widths
+    in 8x8 tiles (96, 128: the tiled decomposition, with a ragged last tile row at H = 50) and
+    not (100: row-major pixels)."""
     s, m = G.scene("huge")
     H, spp = 50, 4
-    monkeypatch.setenv("RT_TILE_LW", "3")
-    base, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, full_frame=True))
-    monkeypatch.setenv("RT_TILE_LW", tile_lw)
     whole, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, full_frame=True))
-    _bits_equal(whole, base)
+    cam = O.camera_default(W, H)
+    for y in (0, 47, 48, 49):  # the tiled rows and the row-major remainder
+        ref, _ = O.render_f32(s, m, cam, rt.make_params(W, H, spp, row_offset=y, num_rows=1))
+        _bits_equal(whole[y:y + 1], ref)
     for n in (2, 3, 8, 16):
         acc = np.zeros_like(whole)
         for r in range(n):
@@ -210,8 +207,8 @@ def _random_scene(rng, n, spread, center=(0.0, 0.0, 0.0)):
     (5, 300, 4.0, (7.0e5, 0.0, 0.0), abi.RT_CAMERA_CORRECTED),
 ])
 @pytest.mark.parametrize("transpose", ["0", "4", "16"])
-def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, transpose, monkeypatch):
-    monkeypatch.setenv("RT_TRANSPOSE_MAX", transpose)
+def test_cluster_culling_is_bit_exact(seed, n, spread, center, mode, transpose, opts):
+    opts.set(transpose_max=int(transpose))
     rng = np.random.default_rng(seed)
     s, m = _random_scene(rng, n, spread, center)
     W, H, spp = 48, 32, 4
@@ -263,9 +260,9 @@ def _glass_scene(rng, n, spread):
                                                       (8, 500, 14.0, abi.RT_CAMERA_CORRECTED, True),
                                                       (9, 200, 8.0, abi.RT_CAMERA_CORRECTED, True),
                                                       (7, 400, 6.0, abi.RT_CAMERA_REFERENCE, False)])  # dense
-def test_isolated_sphere_shortcut_is_bit_exact(seed, n, spread, mode, taken, monkeypatch):
+def test_isolated_sphere_shortcut_is_bit_exact(seed, n, spread, mode, taken, opts):
     """Paths trapped in small glass balls skip the cluster walk when their segment stays inside
-    an isolated ball (RT_ISO, default on): the same bits as without the shortcut, as brute force
+    an isolated ball (default on; RT_DIAG_NO_SHORTCUT off): the same bits as without the shortcut, as brute force
     and as the oracle, with the deep-path split at 3 segments (the deep launch takes the
     shortcut too); the instrumented kernel shows lanes taking it."""
     rng = np.random.default_rng(seed)
@@ -273,12 +270,11 @@ def test_isolated_sphere_shortcut_is_bit_exact(seed, n, spread, mode, taken, mon
     W, H, spp = 48, 32, 8
     cam = O.camera_default(W, H, mode)
     p = rt.make_params(W, H, spp, 64, seed)
-    monkeypatch.setenv("RT_DEEP_MIN_ITEMS", "0")
-    monkeypatch.setenv("RT_DEEP_SPLIT", "3")
+    opts.set(deep_min_items=0, deep_split=3)
     on, st = rt.render_f32((s, m), p, cam)
-    monkeypatch.setenv("RT_ISO", "0")
+    opts.set(no_shortcut=True)
     off, so = rt.render_f32((s, m), p, cam)
-    monkeypatch.delenv("RT_ISO")
+    opts.set(no_shortcut=False)
     _bits_equal(on, off)
     assert st.segments == so.segments
     assert st.box_tests <= so.box_tests
@@ -291,8 +287,7 @@ def test_isolated_sphere_shortcut_is_bit_exact(seed, n, spread, mode, taken, mon
     assert st.segments == seg == sb.segments
     # the instrumented kernel: lanes took the shortcut, and whole iterations skipped the walk
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("RT_DEBUG_STATS", "1")
-    ds = rt.DeviceScene((s, m))
+    ds = rt.DeviceScene((s, m), options=rt.options(rt.default_options(), stats=True))
     out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
     ds.render(rt.Camera.default(W, H, mode), p, out.data_ptr(), stream)
@@ -347,60 +342,54 @@ def test_render_multi_matches_single(ngpu):
 
 
 @pytest.mark.parametrize("spp", [9, 16])
-def test_multi_pass_slots_bit_exact(spp, monkeypatch):
+def test_multi_pass_slots_bit_exact(spp, opts):
     """A slot workspace smaller than the frame's slots forces several render passes whose
     partial sums are carried between passes; the addition order, hence the bits, must not
     change (config 5 at 1024 spp needs two passes)."""
     s, m = G.scene("huge")
     W, H = 64, 32
     one, st1 = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 3))
-    monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * 2))  # 2 slots per pass
+    opts.set(max_pass_bytes=W * H * 12 * 2)  # 2 slots per pass
     many, stn = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 3))
     _bits_equal(many, one)
     assert stn.segments == st1.segments
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk,budget_samples,shade_lds", [(64, 0, "1"), (128, 0, "0"), (512, 0, ""), (8192, 0, "0"),
-                                                           (64, 4, ""), (512, 8, "1"), (192, 12, "0")])
-def test_chunking_and_passes_bit_exact(chunk, budget_samples, shade_lds, monkeypatch):
-    """Items (one sample of one pixel) are dealt in fixed chunks (RT_SCHED=fixed,
-    RT_CHUNK_ITEMS), a small slot budget (RT_SLOT_BUDGET_BYTES) cuts the samples into passes of
-    a multiple of 4, and the shading records may sit in LDS or global memory (RT_SHADE_LDS);
-    none of it may change the bits: the oracle's frame for spp = 23 (5 blocks of 4 + a 3-sample
-    tail). The default guided dealing is covered by every other test and
-    test_guided_dealing_bit_exact."""
-    monkeypatch.setenv("RT_SCHED", "fixed")
+@pytest.mark.parametrize("budget_samples,shade", [(0, "shade_lds"), (0, "shade_global"), (0, ""), (4, ""),
+                                                  (8, "shade_lds"), (12, "shade_global")])
+def test_passes_and_shading_placement_bit_exact(budget_samples, shade, opts):
+    """A small pass size (rt_options.max_pass_bytes) cuts the samples into passes of a multiple
+    of 4, and the shading records may sit in LDS or global memory (RT_DIAG_SHADE_LDS /
+    RT_DIAG_SHADE_GLOBAL); none of it may change the bits: the oracle's frame for spp = 23 (5
+    blocks of 4 + a 3-sample tail)."""
     s, m = G.scene("huge")
     W, H, spp = 40, 24, 23
     p = rt.make_params(W, H, spp, 64, 11)
     cam = O.camera_default(W, H, abi.RT_CAMERA_REFERENCE)
     want, want_seg = O.render_f32(s, m, cam, p)
-    monkeypatch.setenv("RT_CHUNK_ITEMS", str(chunk))
-    monkeypatch.setenv("RT_SHADE_LDS", shade_lds)
+    if shade:
+        opts.set(**{shade: True})
     if budget_samples:
-        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_samples))
+        opts.set(max_pass_bytes=W * H * 12 * budget_samples)
     got, st = rt.render_f32((s, m), p)
     _bits_equal(got, want)
     assert st.segments == want_seg
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("budget_samples,depth,ws,grid", [
-    (0, "2", "1", ""), (4, "2", "1", ""), (0, "3", "2", ""), (4, "3", "2", ""), (4, "4", "2", "2"),
-    (0, "3", "1", "1"), (4, "0", "2", "")])
-def test_frames_in_flight_match_serial(budget_samples, depth, ws, grid, monkeypatch):
-    """Consecutive rt_render_device calls on one scene overlap (render passes on RT_PIPELINE
-    internal streams, RT_WS_PER_STREAM workspaces per stream, partial grids while other renders
-    run); every frame must still equal its serial render, with different cameras, spp and row
-    partitions back to back and no sync between calls, in one pass per frame or in passes of 4
-    samples."""
+@pytest.mark.parametrize("budget_samples,streams,ws", [
+    (0, 2, 1), (4, 2, 1), (0, 3, 2), (4, 3, 2), (4, 4, 2), (0, 7, 2), (4, 8, 1), (4, 1, 2)])
+def test_frames_in_flight_match_serial(budget_samples, streams, ws, opts):
+    """Consecutive rt_render_device calls on one scene overlap (render passes on
+    rt_options.render_streams internal streams with workspaces_per_stream workspaces each,
+    partial grids while other renders run); every frame must still equal its serial render,
+    with different cameras, spp and row partitions back to back and no sync between calls, in
+    one pass per frame or in passes of 4 samples."""
     import torch
-    monkeypatch.setenv("RT_PIPELINE", depth)
-    monkeypatch.setenv("RT_WS_PER_STREAM", ws)
-    monkeypatch.setenv("RT_GRID_WG_PER_CU", grid)
+    opts.set(render_streams=streams, workspaces_per_stream=ws)
     if budget_samples:
-        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(48 * 32 * 12 * budget_samples))
+        opts.set(max_pass_bytes=48 * 32 * 12 * budget_samples)
     s, m = G.scene("huge")
     W, H = 48, 32
     jobs = [(rt.make_params(W, H, 8, 64, 1), O.camera_default(W, H, abi.RT_CAMERA_REFERENCE), H),
@@ -459,13 +448,13 @@ def test_cuda_impl_replacement_u8():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cluster_size", ["4", "8", "12", "24", "32", "64"])
-@pytest.mark.parametrize("transpose", ["0", "16"])
-def test_cluster_size_bit_exact(cluster_size, transpose, monkeypatch):
-    """Any cluster size (RT_CLUSTER_SIZE, read when the scene is created) gives the oracle's
-    bits, with members tested per lane or transposed (clusters above 16 members always per lane)."""
-    monkeypatch.setenv("RT_CLUSTER_SIZE", cluster_size)
-    monkeypatch.setenv("RT_TRANSPOSE_MAX", transpose)
+@pytest.mark.parametrize("cluster_size", [4, 8, 12, 24, 32, 64])
+@pytest.mark.parametrize("transpose", [0, 16])
+def test_cluster_size_bit_exact(cluster_size, transpose, opts):
+    """Any cluster size (rt_options.cluster_size, read when the scene is created) gives the
+    oracle's bits, with members tested per lane or transposed (clusters above 16 members always
+    per lane)."""
+    opts.set(cluster_size=cluster_size, transpose_max=transpose)
     rng = np.random.default_rng(11)
     for s, m in (G.scene("huge"), _random_scene(rng, 900, 10.0)):
         W, H, spp = 40, 24, 4
@@ -479,9 +468,9 @@ def test_cluster_size_bit_exact(cluster_size, transpose, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("transpose", ["0", "16"])
-def test_many_clusters_bit_exact(transpose, monkeypatch):
+def test_many_clusters_bit_exact(transpose, opts):
     """A scene with more than 128 clusters (5000 spheres) gives the oracle's bits."""
-    monkeypatch.setenv("RT_TRANSPOSE_MAX", transpose)
+    opts.set(transpose_max=int(transpose))
     rng = np.random.default_rng(5)
     s, m = _random_scene(rng, 5000, 40.0)
     W, H, spp = 32, 24, 2
@@ -494,16 +483,18 @@ def test_many_clusters_bit_exact(transpose, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,W,H,spp,budget_samples", [("4", 96, 40, 9, 0), ("1", 64, 33, 5, 0), ("0.25", 50, 31, 7, 0),
-                                                      ("16", 96, 40, 8, 4), ("4", 8, 8, 1, 0), ("4", 200, 100, 3, 0)])
-def test_guided_dealing_bit_exact(k, W, H, spp, budget_samples, monkeypatch):
-    """Guided dealing (the default) at several RT_GUIDED_K: each of the 8 queues owns 1/8 of the 64-item blocks and ticket t takes
-    blocks [S(t), S(t+1)), chunks shrinking geometrically to 2 blocks. Every item must be dealt
-    exactly once: the oracle's bits and segment count, in one pass or several, for tiny
-    launches (one wave) and ragged sizes."""
-    monkeypatch.setenv("RT_GUIDED_K", k)
+@pytest.mark.parametrize("streams,W,H,spp,budget_samples", [(0, 96, 40, 9, 0), (1, 64, 33, 5, 0), (0, 50, 31, 7, 0),
+                                                            (0, 96, 40, 8, 4), (1, 8, 8, 1, 0), (2, 200, 100, 3, 0),
+                                                            (1, 96, 40, 8, 4)])
+def test_guided_dealing_bit_exact(streams, W, H, spp, budget_samples, opts):
+    """Guided dealing: each of the 8 queues owns 1/8 of the 64-item blocks and ticket t takes
+    blocks [S(t), S(t+1)), chunks shrinking geometrically to 2 blocks (K = 12 for a pass issued
+    alone, 6 beside other renders). Every item must be dealt exactly once: the oracle's bits and
+    segment count, in one pass or several, on the caller's stream or the render streams, for
+    tiny launches (one wave) and ragged sizes."""
+    opts.set(render_streams=streams)
     if budget_samples:
-        monkeypatch.setenv("RT_SLOT_BUDGET_BYTES", str(W * H * 12 * budget_samples))
+        opts.set(max_pass_bytes=W * H * 12 * budget_samples)
     s, m = G.scene("huge")
     cam = O.camera_default(W, H, abi.RT_CAMERA_REFERENCE)
     p = rt.make_params(W, H, spp, 64, 21)

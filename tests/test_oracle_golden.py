@@ -97,9 +97,16 @@ def _fullframe():
 
 def test_fullframe_digests_cover_the_baseline_configs():
     """tests/golden/fullframe.json holds the reference's own whole-frame digests of BASELINE
-    configs 2 and 3 (and 4, 5 once generated): one 64-bit digest per row, every row present."""
+    configs 2, 3, 4 and 5 (the GPU frame tests compare whole frames against every one of them,
+    so a missing digest must fail here, not skip there): one 64-bit digest per row, every row
+    present, at the BASELINE sizes."""
     ff = _fullframe()
-    assert {"c2", "c3"} <= set(ff)
+    assert {"c2", "c3", "c4", "c5"} <= set(ff)
+    sizes = {"c2": (1280, 720, 64, 50), "c3": (1280, 720, 128, 64), "c4": (3840, 2160, 256, 64),
+             "c5": (1280, 720, 1024, 64)}
+    for name, (W, H, spp, depth) in sizes.items():
+        r = ff[name]
+        assert (r["width"], r["height"], r["spp"], r["depth"]) == (W, H, spp, depth), name
     for name, r in ff.items():
         assert len(r["row_sha256_16"]) == r["height"] and len(r["sha256_f32"]) == 64
         assert r["seed"] == 1234 and r["camera"] == "reference" and r["rng"] == "pcg"

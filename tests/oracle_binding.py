@@ -12,7 +12,8 @@ import numpy as np
 from raytracinginoneweekend_amd import _abi as abi
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(REPO, "oracle", "_build", "librt_oracle.so")
+# RT_ORACLE_SO: a sanitizer build of the same restatement (tests/test_sanitize_cpu.py)
+ORACLE_SO = os.environ.get("RT_ORACLE_SO") or os.path.join(REPO, "oracle", "_build", "librt_oracle.so")
 REF_DIR = os.path.join(REPO, "oracle", "_ref")
 
 _lib = None

@@ -897,6 +897,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 // SIMD's other waves (config 3's 8-way share, split, 7 streams: 0.513-0.515 ms vs
                 // 0.569-0.571; profiles/r03/ab/deep_prio.txt)
                 kd.deep_prio = 1u;
+                // rays trapped in shortcut glass balls bounce in the deep kernel's inner loop
+                kd.trap_loop = (O.diag & RT_DIAG_NO_TRAP_LOOP) ? 0u : 1u;
                 // the shading records in LDS for the deep launch of a pass issued alone: its
                 // paths bounce in glass and shade every segment, and its few busy waves wait on
                 // each global round trip (config 3 single frame: deep launch 0.59 vs 0.65 ms).

@@ -1014,11 +1014,21 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     // its hint sphere (hint_candidate): the geo entry from the shading record
                     const uint32_t hid = P.deep.hid[I], sl = thread_slot(wave_base);
                     if (hid != ~0u) {
+                        // (from LDS when the launch staged the shading records there: a lone
+                        // deep launch, whose refills then wait on no second global round trip)
                         const uint32_t ib = hid & 0x7fffffffu;
-                        const float4 sf = gld4(P.blob + P.shade_offset, 2u * ib);
-                        lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);
                         const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
-                        lds_nb[sl] = __float_as_uint(gld4(P.blob, di).w);
+                        float4 sf, dr;
+                        if (P.shade_lds) {
+                            sf = blob[P.shade_offset + 2u * ib];
+                            dr = blob[di];
+                            asm volatile("");
+                        } else {
+                            sf = gld4(P.blob + P.shade_offset, 2u * ib);
+                            dr = gld4(P.blob, di);
+                        }
+                        lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);
+                        lds_nb[sl] = __float_as_uint(dr.w);
                     }
                     lds_hid[sl] = hid;
                 } else {
@@ -1200,7 +1210,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
             // hid: ~0 = no hint sphere (its top bit is set too), else the sphere's index with
             // kShortcut when the host proved its shortcut
             bool trap = alive && !defer && !pend && hid != ~0u && (hid & kShortcut) && depth < P.max_depth &&
-                        P.iso != 0u;
+                        P.iso != 0u && P.trap_loop != 0u;
             if (lanes(trap) >= kTrapMin) {
                 // S: its geo entry {C, fl(r r)} and shortcut word wait in the lane's LDS slots, its
                 // shading records in the blob (LDS for a lone deep launch, else global memory)

@@ -1204,7 +1204,10 @@ __device__ __forceinline__ void render_body(const KParams &p)
         // closest hit is not S leaves the loop with its state untouched, and the general
         // iteration traces that segment again (same operations, same bits). The wave stays in
         // the loop while its trapped lanes outnumber the waiting ones kTrapWait to one.
-        if constexpr (DEEP && CULL == 7) {
+#ifndef RT_TRAP_MAIN
+#define RT_TRAP_MAIN 0  // the trapped-ray loop in the main kernel too (for passes that are not split)
+#endif
+        if constexpr ((DEEP || RT_TRAP_MAIN) && CULL == 7) {
             const uint32_t sl = thread_slot(wave_base);
             const uint32_t hid = lds_hid[sl];
             // hid: ~0 = no hint sphere (its top bit is set too), else the sphere's index with
@@ -1215,17 +1218,21 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 // S: its geo entry {C, fl(r r)} and shortcut word wait in the lane's LDS slots, its
                 // shading records in the blob (LDS for a lone deep launch, else global memory)
                 const uint32_t sid = trap ? (hid & 0x7fffffffu) : 0u;  // < n_spheres for every lane
+                // (the centre is the geo entry's; of S's first shading record only the signed
+                // radius is kept, of its dielectric record the constants: the shortcut word is
+                // the lane's LDS word)
                 const float4 sg = lds_pn[sl];
                 const uint32_t nbw = lds_nb[sl];
-                float4 sf, md;
+                float sr;
+                float4 md;
                 if (P.shade_lds) {
                     const float4 *shade = blob + P.shade_offset;
-                    sf = shade[2 * sid];
+                    sr = shade[2 * sid].w;
                     md = shade[2 * sid + 1];
                     asm volatile("");
                 } else {
                     const float4 *shade = P.blob + P.shade_offset;
-                    sf = gld4(shade, 2 * sid);
+                    sr = gld4(shade, 2 * sid).w;
                     md = gld4(shade, 2 * sid + 1);
                 }
                 const float4 dcs = dielectric_record<V>(P, blob, sid);
@@ -1266,10 +1273,10 @@ __device__ __forceinline__ void render_body(const KParams &p)
                             // S's dielectric scatter: the general shading's operations, in its order
                             const float t = h.t();
                             const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
-                            const f3 dv = hp - mk(sf.x, sf.y, sf.z);
+                            const f3 dv = hp - mk(sg.x, sg.y, sg.z);
                             f3 hn;
-                            if (P.fast_roots && all_lanes_min_abs_ok(dv)) hn = div3_short(dv, sf.w);  // :71
-                            else hn = dv / sf.w;
+                            if (P.fast_roots && all_lanes_min_abs_ok(dv)) hn = div3_short(dv, sr);  // :71
+                            else hn = dv / sr;
                             att = att * mk(md.x, md.y, md.z);           // main.cxx:65
                             o = hp;
                             f3 ud;

@@ -174,13 +174,12 @@ enum rt_diag {
     RT_DIAG_STANDIN_TRANSPORT = 1u << 9, /* rt_multi with every rank on one device: the RCCL
                                           gather code path, RCCL replaced by stream-ordered
                                           device copies (tests of that path on one GPU)       */
-    RT_DIAG_NO_TRAP_LOOP = 1u << 10,   /* the deep launch without its trapped-ray inner loop  */
-    RT_DIAG_NO_LONE_CUT = 1u << 11     /* a lone frame in one pass (not cut into up to 4)     */
+    RT_DIAG_NO_TRAP_LOOP = 1u << 10    /* the deep launch without its trapped-ray inner loop  */
 };
 int rt_options_default(rt_options *out);
 /* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,
  * no_neighbours, no_root_box, shade_lds, shade_global, stats, stats_deep_only, verbose,
- * standin_transport, no_trap_loop, no_lone_cut = 0/1) to *inout; RT_ERR_INVALID on an unknown key or a
+ * standin_transport, no_trap_loop = 0/1) to *inout; RT_ERR_INVALID on an unknown key or a
  * bad value.                                                                           */
 int rt_options_parse(const char *text, rt_options *inout);
 /* The options of scenes created without explicit ones (NULL: the library defaults).      */

@@ -90,8 +90,6 @@ float guided_l2b(uint32_t total_waves, bool in_flight)
 // the third applies to short passes only. Round 3 re-swept 3/5/7 (7 streams): the default best
 // or within noise (profiles/r03/ab/knobs_s3.txt).
 constexpr uint64_t kShortPassItems = 32ull << 20;
-// a lone frame is cut into at most this many passes (render_device_impl)
-constexpr uint32_t kLoneCut = 4;
 int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams, uint64_t pass_items)
 {
     if (!in_flight) return occ;
@@ -749,21 +747,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     }
     const bool pipe = bufs > 1;
     const uint32_t n_ws = n_ws_of(bufs, wsps);
-    // A frame issued while no other render runs (a lone frame) of a culled scene is cut into up
-    // to kLoneCut passes of a multiple of 4 samples on the render streams: each pass's deep
-    // launch and drain then overlap the next passes' bulk, and only the last pass's tail is
-    // serial (the multi-pass sums keep the reduce order: same bits). A frame in a stream is not
-    // cut (the other frames fill its tail). RT_DIAG_NO_LONE_CUT keeps one pass (A/B).
-    const bool lone = pipe && !(sc->last_ws >= 0 && hipEventQuery(sc->ev_done[sc->last_ws]) == hipErrorNotReady);
-    bool cut = false;
-    if (lone && may_split && !(O.diag & RT_DIAG_NO_LONE_CUT) && P.spp >= 8 && n_pixels * P.spp >= O.deep_min_items) {
-        const uint32_t parts = std::min<uint32_t>(kLoneCut, bufs);
-        const uint64_t sp = std::max<uint64_t>(4, ((P.spp + parts - 1) / parts + 3) & ~3ull);
-        if (sp < spp_pass && (!O.max_workspace_bytes || footprint(bufs, wsps, sp) <= O.max_workspace_bytes)) {
-            spp_pass = sp;
-            cut = true;
-        }
-    }
     const uint64_t spe = std::min<uint64_t>(spp_pass, P.spp);
     // under a cap, workspaces left larger (or more numerous) by earlier frames are re-cut once
     if (O.max_workspace_bytes) {
@@ -847,7 +830,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.deep_depth = 0;
         k.deep_mode = 0;
         bool two_part = false;
-        if (may_split && (k.n_items >= O.deep_min_items || in_flight || cut)) {
+        if (may_split && (k.n_items >= O.deep_min_items || in_flight)) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
             const size_t px_bytes = deep_px_bytes(n_pixels);
             void *had = sc->deep[wb];

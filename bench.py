@@ -424,7 +424,7 @@ def main():
     tile = torch.empty((rows, W, 3), dtype=torch.float32, device=dev)
     rgb8 = args.output == "rgb8"
     tile8 = torch.empty((rows, W, 3), dtype=torch.uint8, device=dev) if rgb8 else None
-    gather = FrameGather(tile8 if rgb8 else tile, world, rank, height=H)
+    gather = FrameGather(tile8 if rgb8 else tile, world, rank, height=None if rehearse else H)
     seg = torch.zeros(3, dtype=torch.int64, device=dev)  # segments, sphere tests, box tests
     stream = torch.cuda.current_stream(dev)
 

@@ -171,16 +171,14 @@ enum rt_diag {
     RT_DIAG_STATS = 1u << 6,           /* the instrumented kernel (rt_scene_debug_*)           */
     RT_DIAG_STATS_DEEP_ONLY = 1u << 7, /* with STATS: count the deep launch alone             */
     RT_DIAG_VERBOSE = 1u << 8,         /* print every launch's plan to stderr                 */
-    RT_DIAG_STANDIN_TRANSPORT = 1u << 9, /* rt_multi with every rank on one device: the RCCL
+    RT_DIAG_STANDIN_TRANSPORT = 1u << 9 /* rt_multi with every rank on one device: the RCCL
                                           gather code path, RCCL replaced by stream-ordered
                                           device copies (tests of that path on one GPU)       */
-    RT_DIAG_NO_TRAP_LOOP = 1u << 10    /* the deep launch without its trapped-ray inner loop  */
 };
 int rt_options_default(rt_options *out);
 /* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,
  * no_neighbours, no_root_box, shade_lds, shade_global, stats, stats_deep_only, verbose,
- * standin_transport, no_trap_loop = 0/1) to *inout; RT_ERR_INVALID on an unknown key or a
- * bad value.                                                                           */
+ * standin_transport = 0/1) to *inout; RT_ERR_INVALID on an unknown key or a bad value.   */
 int rt_options_parse(const char *text, rt_options *inout);
 /* The options of scenes created without explicit ones (NULL: the library defaults).      */
 int rt_set_default_options(const rt_options *options);

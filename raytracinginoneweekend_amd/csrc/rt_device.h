@@ -103,7 +103,6 @@ struct KParams {
     uint32_t deep_depth;     // 0: no split (and always 0 in the deep launch)
     uint32_t deep_mode;      // the deep launch: the split depth (its paths resume there); 0 otherwise
     uint32_t deep_prio;      // the deep launch's waves at the highest issue priority (s_setprio 3)
-    uint32_t trap_loop;      // the deep launch's trapped-ray inner loop (render_body)
 };
 
 struct KAccum {

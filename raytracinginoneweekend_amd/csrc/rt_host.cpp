@@ -90,6 +90,10 @@ float guided_l2b(uint32_t total_waves, bool in_flight)
 // the third applies to short passes only. Round 3 re-swept 3/5/7 (7 streams): the default best
 // or within noise (profiles/r03/ab/knobs_s3.txt).
 constexpr uint64_t kShortPassItems = 32ull << 20;
+// the deep launch of a lone pass stages the shading records in LDS (A/B build switch)
+#ifndef RT_DEEP_LDS_STAGE
+#define RT_DEEP_LDS_STAGE 1
+#endif
 int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams, uint64_t pass_items)
 {
     if (!in_flight) return occ;
@@ -897,14 +901,12 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 // SIMD's other waves (config 3's 8-way share, split, 7 streams: 0.513-0.515 ms vs
                 // 0.569-0.571; profiles/r03/ab/deep_prio.txt)
                 kd.deep_prio = 1u;
-                // rays trapped in shortcut glass balls bounce in the deep kernel's inner loop
-                kd.trap_loop = (O.diag & RT_DIAG_NO_TRAP_LOOP) ? 0u : 1u;
                 // the shading records in LDS for the deep launch of a pass issued alone: its
                 // paths bounce in glass and shade every segment, and its few busy waves wait on
                 // each global round trip (config 3 single frame: deep launch 0.59 vs 0.65 ms).
                 // Not beside other renders: its larger workgroups then displace theirs (frame
                 // stream 2.69-2.73 vs 2.57-2.59 ms per frame, 8-way share 0.45 vs 0.42)
-                if (!in_flight && variant != rt::V_EXACT_SCALAR && !k.shade_lds && shade_fits) {
+                if (RT_DEEP_LDS_STAGE && !in_flight && variant != rt::V_EXACT_SCALAR && !k.shade_lds && shade_fits) {
                     kd.shade_lds = 1u;
                     kd.lds_units = k.blob_units;
                 }

@@ -74,8 +74,6 @@ enum DbgEvent : uint32_t {
     EV_DRY_LANES,   // live lanes summed over those
     EV_ISO_LANES,   // lanes that skipped the cluster walk (isolated hint sphere), summed over iterations
     EV_WALK_SKIPPED,  // wave iterations with segments whose cluster walk no lane needed
-    EV_TRAP_ITER,     // iterations of the deep launch's trapped-ray loop
-    EV_TRAP_LANES,    // trapped lanes summed over those
     EV_COUNT
 };
 static_assert(EV_COUNT <= kDbgEvents, "event counters");
@@ -816,16 +814,6 @@ __device__ __forceinline__ float4 dielectric_record(const KP &P, const float4 *b
 #endif
 template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_PER_SIMD;
-// the deep launch's trapped-ray loop (render_body): entered when at least kTrapMin lanes of the
-// wave trace a ray inside a shortcut glass ball, left when the trapped lanes fall below
-// kTrapWait times the lanes waiting for the general iteration
-#ifndef RT_TRAP_MIN
-#define RT_TRAP_MIN 1
-#endif
-#ifndef RT_TRAP_WAIT
-#define RT_TRAP_WAIT 4
-#endif
-constexpr uint32_t kTrapMin = RT_TRAP_MIN, kTrapWait = RT_TRAP_WAIT;
 // The render loop; DEEP: the deep launch of a split pass (KParams::deep_mode),
 // whose items are queued paths (no sample starts, no lens draws, no split) — its own
 // instantiation, render_deep_kernel, so neither launch carries the other's code.
@@ -1192,116 +1180,6 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 }
             }
         }
-        // ---- the deep launch's trapped rays ---------------------------------
-        // 98% of the deep launch's live lanes trace a ray inside a small glass ball S whose walk
-        // shortcut the host has proven (hint_candidate): every segment is S's far wall, the
-        // ground (tested anyway) or one of S's at most two neighbours, and the path stays there
-        // for ~50 bounces (the reference's refract, raytracer.hxx:158-194). Those lanes bounce
-        // in this inner loop with S's records in registers: per segment the candidates of S,
-        // its neighbours and the ground (the general iteration's hint_candidate + the always-
-        // tested list, same ops), and, when S wins, S's dielectric scatter (raytracer.hxx:158-
-        // 194, the general shading's ops). A lane whose segment leaves the ball or whose
-        // closest hit is not S leaves the loop with its state untouched, and the general
-        // iteration traces that segment again (same operations, same bits). The wave stays in
-        // the loop while its trapped lanes outnumber the waiting ones kTrapWait to one.
-#ifndef RT_TRAP_MAIN
-#define RT_TRAP_MAIN 0  // the trapped-ray loop in the main kernel too (for passes that are not split)
-#endif
-        if constexpr ((DEEP || RT_TRAP_MAIN) && CULL == 7) {
-            const uint32_t sl = thread_slot(wave_base);
-            const uint32_t hid = lds_hid[sl];
-            // hid: ~0 = no hint sphere (its top bit is set too), else the sphere's index with
-            // kShortcut when the host proved its shortcut
-            bool trap = alive && !defer && !pend && hid != ~0u && (hid & kShortcut) && depth < P.max_depth &&
-                        P.iso != 0u && P.trap_loop != 0u;
-            if (lanes(trap) >= kTrapMin) {
-                // S: its geo entry {C, fl(r r)} and shortcut word wait in the lane's LDS slots, its
-                // shading records in the blob (LDS for a lone deep launch, else global memory)
-                const uint32_t sid = trap ? (hid & 0x7fffffffu) : 0u;  // < n_spheres for every lane
-                // (the centre is the geo entry's; of S's first shading record only the signed
-                // radius is kept, of its dielectric record the constants: the shortcut word is
-                // the lane's LDS word)
-                const float4 sg = lds_pn[sl];
-                const uint32_t nbw = lds_nb[sl];
-                float sr;
-                float4 md;
-                if (P.shade_lds) {
-                    const float4 *shade = blob + P.shade_offset;
-                    sr = shade[2 * sid].w;
-                    md = shade[2 * sid + 1];
-                    asm volatile("");
-                } else {
-                    const float4 *shade = P.blob + P.shade_offset;
-                    sr = gld4(shade, 2 * sid).w;
-                    md = gld4(shade, 2 * sid + 1);
-                }
-                const float4 dcs = dielectric_record<V>(P, blob, sid);
-                const uint64_t inc_t = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
-                for (;;) {
-                    const uint64_t tm = ballot(trap);
-                    const uint32_t nt = (uint32_t)__popcll(tm);
-                    if (nt == 0u || nt < kTrapWait * lanes(alive && !trap)) break;
-                    if (STATS && first_active_lane()) {
-                        ++dbg.ev[EV_TRAP_ITER];
-                        dbg.ev[EV_TRAP_LANES] += nt;
-                    }
-                    const float a = d.x * d.x + d.y * d.y + d.z * d.z;  // raytracer.hxx:56
-                    const RayDiv rd = ray_div(a, tm, P.fast_roots);
-                    bool inside;
-                    Hit h{hint_candidate<FAST>(trap, sg, hid, nbw, geo, sidx, o, d, rd, 1u, inside)};
-                    if (RT_GROUND1 && P.n_always == 1u) test_block8<FAST, STATS, 1>(geo, sidx, 0, o, d, rd, h, dbg);
-                    else run_members<FAST, STATS>(geo, sidx, 0, P.n_always, o, d, rd, h, dbg);
-                    const bool stay = trap && inside && h.id() == sid;
-                    trap = stay;
-                    {
-                        const uint32_t ns = lanes(stay);  // segments traced here (main.cxx:74 passed)
-                        wt.add_seg(ns);
-                        wt.add_sph((uint64_t)ns * P.n_always);
-                    }
-                    if (stay) {
-                        ++depth;
-                        if (depth >= P.max_depth) {
-                            // main.cxx:65-74: the scattered ray would not be traced; colour 0
-                            trap = alive = false;
-                            float *dst = P.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;
-                            float z = 0.f;
-                            asm volatile("" : "+v"(z));
-                            dst[0] = z;
-                            dst[1] = z;
-                            dst[2] = z;
-                        } else {
-                            // S's dielectric scatter: the general shading's operations, in its order
-                            const float t = h.t();
-                            const f3 hp = o + d * t;                    // ray::point_at, math.hxx:353
-                            const f3 dv = hp - mk(sg.x, sg.y, sg.z);
-                            f3 hn;
-                            if (P.fast_roots && all_lanes_min_abs_ok(dv)) hn = div3_short(dv, sr);  // :71
-                            else hn = dv / sr;
-                            att = att * mk(md.x, md.y, md.z);           // main.cxx:65
-                            o = hp;
-                            f3 ud;
-                            if (rd.fd != 0u && all_lanes_min_abs_ok(d)) ud = div3_short(d, sqrt_scaled(a));
-                            else ud = normalize(d);
-                            const f3 rf = reflect(ud, hn);
-                            f3 outward = mk(-hn.x, -hn.y, -hn.z);
-                            float ri = md.w, xs = dcs.y;
-                            float cosv = dot(ud, hn);
-                            if (cosv <= 0.f) {
-                                outward = outward * -1.f;
-                                ri = dcs.x;
-                                xs = dcs.z;
-                                cosv *= -1.f;
-                            }
-                            const f3 refr = refract(ud, outward, ri);
-                            float prob = 1.f;
-                            if (refr.x * refr.x + refr.y * refr.y + refr.z * refr.z > 0.f) prob = schlick_x(xs, cosv);
-                            d = canonical(rng, inc_t) < prob ? rf : refr;
-                        }
-                    }
-                }
-                if (ballot(alive) == 0) continue;  // every path ended at max_depth: refill
-            }
-        }
         RT_EV(EV_ITER);
         if (STATS) {
             const uint32_t nl = lanes(alive);
@@ -1530,13 +1408,8 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
     render_body<V, CULL, STATS, COUNT, false>(p);
 }
 // the deep launch of a split pass (culled scenes only)
-// The deep kernel holds a trapped ray's sphere records in registers (render_body): 80 VGPRs at
-// 6 waves per SIMD, where the deep launch keeps ~3.4 busy waves per SIMD anyway
-#ifndef RT_DEEP_WAVES
-#define RT_DEEP_WAVES 6
-#endif
 template <int V, bool STATS, bool COUNT>
-__global__ __launch_bounds__(256, (STATS ? 1 : RT_DEEP_WAVES)) void render_deep_kernel(const KParams p)
+__global__ __launch_bounds__(256, (kMinWaves<V, 7, STATS>)) void render_deep_kernel(const KParams p)
 {
     render_body<V, 7, STATS, COUNT, true>(p);
 }

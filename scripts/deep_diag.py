@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""The deep launch of a lone config-3 frame under the instrumented kernel (options stats=1,
+stats_deep_only=1): block events per iteration, cycle shares per loop region, and the per-wave
+timeline (when each wave found the queues dry, exited, its iterations) — for each --options.
+    python scripts/deep_diag.py [--options "no_trap_loop=1" ...]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+import raytracinginoneweekend_amd as rt  # noqa: E402
+from bench import CONFIGS  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c3")
+ap.add_argument("--options", nargs="*", default=[""])
+a = ap.parse_args()
+scene, W, H, spp, depth = CONFIGS[a.config]
+arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
+cam = rt.Camera.default(W, H)
+p = rt.make_params(W, H, spp, depth, 1234)
+out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+stream = torch.cuda.current_stream().cuda_stream
+for text in a.options:
+    o = rt.parse_options(text, rt.options(rt.default_options(), stats=True, stats_deep_only=True))
+    ds = rt.DeviceScene(arrays, options=o)
+    for _ in range(2):  # the second lone frame is reported
+        torch.cuda.synchronize()
+        ds.debug_counters(reset=True)
+        ds.debug_events(reset=True)
+        ds.render(cam, p, out.data_ptr(), stream)
+        torch.cuda.synchronize()
+    c, ev = ds.debug_counters(reset=True), ds.debug_events(reset=True)
+    tl = [r for r in ds.debug_timeline() if r[1] >= r[0] > 0]
+    t0 = c["launch_start"] or (min(r[0] for r in tl) if tl else 0)
+    cyc = sum(c[k] for k in ("cyc_refill", "cyc_start", "cyc_hit", "cyc_shade", "cyc_fold"))
+    busy = [r for r in tl if r[2] > 0]
+    ends = sorted(r[1] - t0 for r in busy)
+    q = lambda v, f: v[min(len(v) - 1, int(f * len(v)))] / 100.0 if v else None  # noqa: E731  (100 MHz ticks -> us)
+    res = {"options": text, "lone_frame_ms": ds.kernel_times(1)[0], "waves": len(tl), "busy_waves": len(busy),
+           "wave_iters": c["wave_iters"], "refills": c["wave_refills"],
+           "cycle_share": {k: round(c[k] / max(1, cyc), 3) for k in ("cyc_refill", "cyc_start", "cyc_hit", "cyc_shade", "cyc_fold")},
+           "cycles_per_wave_iter": round(cyc / max(1, c["wave_iters"]), 1),
+           "events": {k: int(v) for k, v in ev.items() if v},
+           "busy_wave_exit_us": {f"p{int(f * 100)}": q(ends, f) for f in (0.0, 0.1, 0.5, 0.9, 0.99, 1.0)},
+           "iters_per_busy_wave": {f"p{int(f * 100)}": (sorted(r[2] for r in busy)[min(len(busy) - 1, int(f * len(busy)))] if busy else None)
+                                   for f in (0.0, 0.5, 0.9, 1.0)}}
+    print(json.dumps(res), flush=True)
+    ds.close()

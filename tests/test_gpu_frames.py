@@ -293,74 +293,6 @@ def test_deep_split_matches_unsplit(split, opts):
         assert sb.segments == sa.segments and sb.primaries == sa.primaries
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_trapped_ray_loop_matches_general_iteration(mode, opts):
-    """The deep launch's trapped-ray loop (rays bouncing inside shortcut glass balls with the ball's
-    records in registers) against the same deep launch without it (RT_DIAG_NO_TRAP_LOOP): the
-    same frames and segment counts, on the huge scene (split at 2, 3 and 8 segments, lone and
-    streamed passes, shading records in LDS and in global memory) and on glass-ball scenes whose
-    balls touch, overlap, nest a bubble or duplicate each other."""
-    torch = pytest.importorskip("torch")
-    rng = np.random.default_rng(31 + mode)
-    import test_gpu_parity as GP
-    scenes = [G.scene("huge"), GP._glass_scene(rng, 300, 8.0)]
-    stream = torch.cuda.current_stream().cuda_stream
-    for si, (s, m) in enumerate(scenes):
-        for split in (2, 3, 8):
-            W, H, spp = (96, 54, 16) if split == 8 else (64, 36, 8)
-            cam = rt.Camera.default(W, H, mode)
-            p = rt.make_params(W, H, spp, 64, 40 + split)
-            outs = {}
-            for no_trap in (True, False):
-                o = rt.options(rt.default_options(), deep_split=split, deep_min_items=0, no_trap_loop=no_trap)
-                ds = rt.DeviceScene((s, m), options=o)
-                frames, segs = [], []
-                for _ in range(3):  # a lone pass (deep shading in LDS), then passes in flight
-                    frames.append(torch.empty((H, W, 3), dtype=torch.float32, device="cuda"))
-                    segs.append(torch.zeros(3, dtype=torch.int64, device="cuda"))
-                    ds.render(cam, p, frames[-1].data_ptr(), stream, segs[-1].data_ptr())
-                torch.cuda.synchronize()
-                ds.close()
-                outs[no_trap] = [(f.cpu().numpy(), int(g[0])) for f, g in zip(frames, segs)]
-            for (a, sa), (b, sb) in zip(outs[True], outs[False]):
-                _bits_equal(b, a, f"scene {si} split {split} camera {mode}")
-                assert sa == sb
-
-
-@pytest.mark.parametrize("mode", [0, 1])
-def test_trapped_ray_loop_matches_general_iteration(mode, opts):
-    """The deep launch's trapped-ray loop (rays bouncing inside shortcut glass balls with the ball's
-    records in registers) against the same deep launch without it (RT_DIAG_NO_TRAP_LOOP): the
-    same frames and segment counts, on the huge scene (split at 2, 3 and 8 segments, lone and
-    streamed passes, shading records in LDS and in global memory) and on glass-ball scenes whose
-    balls touch, overlap, nest a bubble or duplicate each other."""
-    torch = pytest.importorskip("torch")
-    rng = np.random.default_rng(31 + mode)
-    import test_gpu_parity as GP
-    scenes = [G.scene("huge"), GP._glass_scene(rng, 300, 8.0)]
-    stream = torch.cuda.current_stream().cuda_stream
-    for si, (s, m) in enumerate(scenes):
-        for split in (2, 3, 8):
-            W, H, spp = (96, 54, 16) if split == 8 else (64, 36, 8)
-            cam = rt.Camera.default(W, H, mode)
-            p = rt.make_params(W, H, spp, 64, 40 + split)
-            outs = {}
-            for no_trap in (True, False):
-                o = rt.options(rt.default_options(), deep_split=split, deep_min_items=0, no_trap_loop=no_trap)
-                ds = rt.DeviceScene((s, m), options=o)
-                frames, segs = [], []
-                for _ in range(3):  # a lone pass (deep shading in LDS), then passes in flight
-                    frames.append(torch.empty((H, W, 3), dtype=torch.float32, device="cuda"))
-                    segs.append(torch.zeros(3, dtype=torch.int64, device="cuda"))
-                    ds.render(cam, p, frames[-1].data_ptr(), stream, segs[-1].data_ptr())
-                torch.cuda.synchronize()
-                ds.close()
-                outs[no_trap] = [(f.cpu().numpy(), int(g[0])) for f, g in zip(frames, segs)]
-            for (a, sa), (b, sb) in zip(outs[True], outs[False]):
-                _bits_equal(b, a, f"scene {si} split {split} camera {mode}")
-                assert sa == sb
-
-
 def test_deep_split_against_oracle_and_golden(opts):
     """With the split at 2 segments (most continuing paths go through the deep queue): the
     reference's own frame (golden huge_64x36_s4) and the oracle on a multi-pass render."""

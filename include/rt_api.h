@@ -148,9 +148,9 @@ typedef struct rt_options {
                                        12 B .. 2 GiB (2 GiB); frames above it run in passes    */
     uint64_t max_workspace_bytes;   /* cap on the scene's device workspaces (slots, deep-path
                                        queues, multi-pass sums, wavefront queues); 0 = none.
-                                       Over it, passes shrink (to 4 samples), then workspaces
-                                       per stream, then streams go; RT_ERR_CAPACITY if one
-                                       4-sample pass on the caller's stream does not fit       */
+                                       Over it, workspaces per stream go to 1, then passes
+                                       shrink (to 4 samples), then streams go; RT_ERR_CAPACITY
+                                       if one 4-sample pass on the caller's stream does not fit */
     uint64_t deep_min_items;        /* a pass issued while no other render runs (a lone frame)
                                        is split only from this many samples (2^25); passes
                                        issued beside other renders are split at any size       */

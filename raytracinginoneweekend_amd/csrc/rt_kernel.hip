@@ -511,7 +511,10 @@ __device__ __forceinline__ bool box_pass(const RayBox &r, float4 c0, float4 c1, 
 // per-sphere candidate (near root if in range, else far root, raytracer.hxx:62-90), and the
 // candidates are combined by the (t, original index) minimum as key = bits(t) << 32 | index
 // (t > 0, so the u64 order is that order): the same hit, in any order. Whole-wave code.
-constexpr uint32_t kTransposeMax = 16;  // rays per transposed cluster (KParams::transpose_max <= this)
+#ifndef RT_TRANSPOSE_LDS
+#define RT_TRANSPOSE_LDS 16  // rays per transposed cluster the per-wave LDS holds
+#endif
+constexpr uint32_t kTransposeMax = RT_TRANSPOSE_LDS;  // KParams::transpose_max is clamped to this
 // unsigned minimum over each row of 16 lanes: xor 1, xor 2 (quad permutes), then the half-row
 // mirror and the row mirror leave every lane of a row with the row's minimum
 // (the DPP moves carry the identity of min as their old value, so the compiler folds each into
@@ -622,7 +625,7 @@ __device__ __forceinline__ void cluster_members7(bool req, uint64_t M, uint32_t 
     const uint32_t scu = __builtin_amdgcn_readfirstlane(scu_lane);
     const uint32_t start = scu & 0xffffu, cnt = scu >> 16;
     wt.add_sph((uint64_t)__popcll(M) * cnt);
-    if ((uint32_t)__popcll(M) <= tmax && cnt <= 16u) {
+    if ((uint32_t)__popcll(M) <= min(tmax, kTransposeMax) && cnt <= 16u) {
         RT_EV(EV_TRANSPOSED);
         members_transposed<FAST, STATS>(geo, sidx, start, cnt, M, req, tw, o, d, rd, h, dbg);
     } else if (req) {

@@ -91,6 +91,10 @@ float guided_l2b(uint32_t total_waves, bool in_flight)
 // or within noise (profiles/r03/ab/knobs_s3.txt).
 constexpr uint64_t kShortPassItems = 32ull << 20;
 // the deep launch of a lone pass stages the shading records in LDS (A/B build switch)
+// lone split passes accumulate in two parts, the first beside the deep launch (A/B build switch)
+#ifndef RT_TWO_PART
+#define RT_TWO_PART 1
+#endif
 #ifndef RT_DEEP_LDS_STAGE
 #define RT_DEEP_LDS_STAGE 1
 #endif
@@ -860,7 +864,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             k.deep.ctr = k.queue_ctr;
             k.deep.rcap = rcap;
             k.deep_depth = deep_split;
-            two_part = pipe && !in_flight;
+            two_part = RT_TWO_PART && pipe && !in_flight;
         }
         if (O.diag & RT_DIAG_VERBOSE)
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u "

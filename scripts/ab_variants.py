@@ -25,12 +25,14 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--depth", type=int, default=0, help="override the config's max depth")
+ap.add_argument("--spp", type=int, default=0, help="override the config's samples per pixel")
 ap.add_argument("--variants", default="exact:cull,exact:brute,fast:cull,fast:brute")
 ap.add_argument("--stats", action="store_true", help="the instrumented kernel (counters and per-wave timeline)")
 ap.add_argument("--timeline-out", default="", help="with --stats: dump raw per-wave records to <prefix>.<variant>.json")
 a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
 depth = a.depth or depth
+spp = a.spp or spp
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H, rt.CORRECTED if a.camera == "corrected" else rt.REFERENCE)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")

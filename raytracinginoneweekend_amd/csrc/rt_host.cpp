@@ -29,7 +29,8 @@
 using namespace rthost;
 
 namespace rt {
-hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream);
+hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream, int wpb = 4);
+hipError_t deep_occupancy(int variant, int wpb, size_t lds, int *blocks_per_cu, size_t *static_lds);
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
 hipError_t static_lds_render(int variant, int cull, size_t *bytes);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
@@ -98,6 +99,14 @@ constexpr uint64_t kShortPassItems = 32ull << 20;
 #ifndef RT_DEEP_LDS_STAGE
 #define RT_DEEP_LDS_STAGE 1
 #endif
+// ... in 8-wave workgroups (one LDS copy of the scene for twice the waves), every workgroup
+// resident at once, dealing the queued paths statically (A/B build switches)
+#ifndef RT_DEEP_WIDE
+#define RT_DEEP_WIDE 1
+#endif
+#ifndef RT_DEEP_STATIC
+#define RT_DEEP_STATIC 1
+#endif
 int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams, uint64_t pass_items)
 {
     if (!in_flight) return occ;
@@ -162,6 +171,9 @@ struct rt_scene {
     bool tail_valid = false;
     int cu_count = 0;
     int occ[4][2][2];  // [variant][culled][shade records in LDS] blocks per CU, -1 = unknown
+    // [variant] blocks per CU of the 8-wave deep kernel with the whole blob in LDS, -1 = unknown,
+    // 0 = it does not fit or holds no more waves than 4-wave groups (the lone deep launch)
+    int occ_deep_wide[4] = {-1, -1, -1, -1};
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DIAG_STATS)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
@@ -843,6 +855,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.deep_depth = 0;
         k.deep_mode = 0;
         bool two_part = false;
+        uint32_t stats_waves = 0;  // the instrumented build: waves of the launch the counters cover
         if (may_split && (k.n_items >= O.deep_min_items || in_flight)) {
             const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
             const size_t px_bytes = deep_px_bytes(n_pixels);
@@ -893,6 +906,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             }
         } else {
             RT_HIP(rt::launch_render(variant, cull_mode, k, grid, xst));
+            stats_waves = grid * 4u;
             if (two_part) {
                 if (!sc->ev_main[wb]) RT_HIP(hipEventCreateWithFlags(&sc->ev_main[wb], hipEventDisableTiming));
                 RT_HIP(hipEventRecord(sc->ev_main[wb], xst));
@@ -915,19 +929,39 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 // each global round trip (config 3 single frame: deep launch 0.59 vs 0.65 ms).
                 // Not beside other renders: its larger workgroups then displace theirs (frame
                 // stream 2.69-2.73 vs 2.57-2.59 ms per frame, 8-way share 0.45 vs 0.42)
+                int wpb = 4;
+                uint32_t dgrid = grid;
                 if (RT_DEEP_LDS_STAGE && !in_flight && variant != rt::V_EXACT_SCALAR && !k.shade_lds && shade_fits) {
                     kd.shade_lds = 1u;
                     kd.lds_units = k.blob_units;
+                    // 8-wave groups share the LDS copy (3 x 8 waves per CU instead of 3 x 4), the
+                    // grid is what is resident at once, and the chunks are dealt statically: the
+                    // launch was ~0.28 ms even for paths of one segment, most of it thousands of
+                    // waves probing the regions' counters and groups waiting for residency
+                    int &ow = sc->occ_deep_wide[variant];
+                    if (ow < 0) {
+                        const size_t bytes = static_cast<size_t>(k.blob_units) * 16u;
+                        size_t st8 = 0;
+                        int o8 = 0;
+                        RT_HIP(rt::deep_occupancy(variant, 8, bytes, &o8, &st8));
+                        ow = bytes + st8 <= sc->max_lds && o8 * 8 > occ_all * 4 ? o8 : 0;
+                    }
+                    if (RT_DEEP_WIDE && ow > 0) {
+                        wpb = 8;
+                        dgrid = static_cast<uint32_t>(ow * sc->cu_count);
+                        kd.deep_static = RT_DEEP_STATIC ? 1u : 0u;
+                    }
                 }
                 if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) {
                     // diagnostics: the counters and events of the deep launch alone
                     RT_HIP(hipMemsetAsync(sc->dbg, 0, 16 * sizeof(unsigned long long), xst));
                     RT_HIP(hipMemsetAsync(sc->dbg + rt::kDbgEvBase, 0, rt::kDbgEvents * sizeof(unsigned long long), xst));
                 }
-                RT_HIP(rt::launch_render(variant, cull_mode, kd, grid, xst));
+                RT_HIP(rt::launch_render(variant, cull_mode, kd, dgrid, xst, wpb));
+                if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) stats_waves = dgrid * static_cast<uint32_t>(wpb);
             }
         }
-        if (variant == rt::V_STATS_LDS) sc->dbg_waves = grid * 4u;
+        if (variant == rt::V_STATS_LDS) sc->dbg_waves = stats_waves;
         if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], xst));
         if (pipe) {
             RT_HIP(hipEventRecord(sc->ev_done[wb], xst));

@@ -820,7 +820,9 @@ constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_
 // The render loop; DEEP: the deep launch of a split pass (KParams::deep_mode),
 // whose items are queued paths (no sample starts, no lens draws, no split) — its own
 // instantiation, render_deep_kernel, so neither launch carries the other's code.
-template <int V, int CULL, bool STATS, bool COUNT, bool DEEP>
+// WPB: waves per workgroup (4; the lone deep launch 8, which shares one LDS copy of the scene
+// between twice the waves)
+template <int V, int CULL, bool STATS, bool COUNT, bool DEEP, int WPB>
 __device__ __forceinline__ void render_body(const KParams &p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
@@ -853,14 +855,14 @@ __device__ __forceinline__ void render_body(const KParams &p)
     // per-wave LDS of the transposed member tests
     TransposeLds *tw = nullptr;
     if constexpr (CULL == 7) {
-        __shared__ TransposeLds s_tw[4];
+        __shared__ TransposeLds s_tw[WPB];
         tw = &s_tw[threadIdx.x >> 6];
     }
     // per lane: a pending metal scatter's normal and roughness, or the geo entry {C, fl(r r)} of
     // the dielectric sphere the lane's path last hit (hint_candidate; its original index in lds_hid)
-    __shared__ float4 lds_pn[256];
-    __shared__ uint32_t lds_hid[256];
-    __shared__ uint32_t lds_nb[256];  // the dielectric sphere's shortcut word (hint_candidate)
+    __shared__ float4 lds_pn[64 * WPB];
+    __shared__ uint32_t lds_hid[64 * WPB];
+    __shared__ uint32_t lds_nb[64 * WPB];  // the dielectric sphere's shortcut word (hint_candidate)
     const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
     // the deep launch's waves issue ahead of other launches' waves (KParams::deep_prio): each of
@@ -869,6 +871,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
     if (DEEP && p.deep_prio) __builtin_amdgcn_s_setprio(3);
     // wave-uniform cursor over the item space (the deep launch: over the queued paths)
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
+    // static dealing (KParams::deep_static): this wave's next chunk of the deep queue, in the
+    // order of the regions' chunks; the grid's waves take chunks w, w + waves, w + 2 waves, ...
+    uint32_t deep_next = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + (threadIdx.x >> 6));
     uint32_t cnext = 0, cend = 0;
     bool exhausted = false;
 
@@ -943,6 +948,35 @@ __device__ __forceinline__ void render_body(const KParams &p)
             if (cnext >= cend) {
                 uint32_t c = 0;
                 if constexpr (DEEP) {
+                    if (WPB == 8 && P.deep_static) {  // (the lone deep launch's instantiation only)
+                        // the regions' path counts are final (the main launch has ended): lanes
+                        // 0-7 read them in one round trip; chunk j of the concatenated regions
+                        // goes to wave j mod waves. No atomics: thousands of waves probing eight
+                        // shared counters at the end of a launch cost more than the paths
+                        const uint32_t n = lane < 8u ? min(P.deep.ctr[lane * kQueueStride + kDeepCount], P.deep.rcap) : 0u;
+                        const uint32_t j = deep_next;
+                        deep_next += gridDim.x * (uint32_t)WPB;
+                        // lane k < 8: region k's chunks and their first index (exclusive prefix
+                        // over lanes 0..k-1, three shuffle steps); the region holding chunk j
+                        const uint32_t ck = (n + 63u) / 64u;
+                        uint32_t incl = ck;
+#pragma unroll
+                        for (uint32_t off = 1; off < 8u; off <<= 1) {
+                            const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
+                            if (lane >= off) incl += v;
+                        }
+                        const uint64_t hit = ballot(lane < 8u && j < incl && j >= incl - ck);
+                        if (!hit) {
+                            exhausted = true;
+                            continue;
+                        }
+                        const uint32_t r = (uint32_t)__builtin_ctzll(hit);
+                        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)(incl - ck), (int)r);
+                        const uint32_t nr = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)r);
+                        cnext = r * P.deep.rcap + 64u * (j - base);
+                        cend = r * P.deep.rcap + min(64u * (j - base) + 64u, nr);
+                        goto deal;
+                    }
                     // the deep launch: 64 queued paths per grab from region q, then the next
                     // region (a wave starts on its workgroup's region)
                     if (lane == 0) c = atomicAdd(P.deep.ctr + q * kQueueStride + kDeepDeal, 1u);
@@ -983,6 +1017,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), P.n_items));
                 }
             }
+        deal:
             const uint32_t avail = cend - cnext;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -1408,13 +1443,14 @@ __device__ __forceinline__ void render_body(const KParams &p)
 template <int V, int CULL, bool STATS, bool COUNT>
 __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kernel(const KParams p)
 {
-    render_body<V, CULL, STATS, COUNT, false>(p);
+    render_body<V, CULL, STATS, COUNT, false, 4>(p);
 }
-// the deep launch of a split pass (culled scenes only)
-template <int V, bool STATS, bool COUNT>
-__global__ __launch_bounds__(256, (kMinWaves<V, 7, STATS>)) void render_deep_kernel(const KParams p)
+// the deep launch of a split pass (culled scenes only); WPB = 8: the lone deep launch with the
+// shading records in LDS, whose workgroups per CU the LDS bounds
+template <int V, bool STATS, bool COUNT, int WPB>
+__global__ __launch_bounds__(64 * WPB, (WPB == 8 && !STATS ? 6 : kMinWaves<V, 7, STATS>)) void render_deep_kernel(const KParams p)
 {
-    render_body<V, 7, STATS, COUNT, true>(p);
+    render_body<V, 7, STATS, COUNT, true, WPB>(p);
 }
 
 // ---- the reference's CUDA variant (RT_FLAG_CUDA_COMPAT) -----------------------------------
@@ -1915,27 +1951,44 @@ static const void *render_ptr(int variant, int cull, bool count)
     return count ? render_ptr_c<true>(variant, cull) : render_ptr_c<false>(variant, cull);
 }
 
-template <bool COUNT> static const void *render_deep_ptr_c(int variant)
+template <bool COUNT, int WPB> static const void *render_deep_ptr_w(int variant)
 {
     switch (variant) {
-    case V_EXACT_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_EXACT_LDS, false, COUNT>);
-    case V_FAST_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_FAST_LDS, false, COUNT>);
-    case V_STATS_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_EXACT_LDS, true, true>);
+    case V_EXACT_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_EXACT_LDS, false, COUNT, WPB>);
+    case V_FAST_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_FAST_LDS, false, COUNT, WPB>);
+    case V_STATS_LDS: return reinterpret_cast<const void *>(&render_deep_kernel<V_EXACT_LDS, true, true, WPB>);
     default: return nullptr;
     }
 }
-
-hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream)
+static const void *render_deep_ptr(int variant, bool count, int wpb)
 {
-    // the deep launch (deep_mode != 0) exists for culled scenes only
+    if (wpb == 8) return count ? render_deep_ptr_w<true, 8>(variant) : render_deep_ptr_w<false, 8>(variant);
+    if (wpb == 4) return count ? render_deep_ptr_w<true, 4>(variant) : render_deep_ptr_w<false, 4>(variant);
+    return nullptr;
+}
+
+hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream, int wpb)
+{
+    // the deep launch (deep_mode != 0) exists for culled scenes only; only it has 8-wave groups
     const bool count = p.segments != nullptr;
-    const void *fn = p.deep_mode ? (cull == 7 ? (count ? render_deep_ptr_c<true>(variant) : render_deep_ptr_c<false>(variant))
-                                              : nullptr)
-                                 : render_ptr(variant, cull, count);
+    const void *fn = p.deep_mode ? (cull == 7 ? render_deep_ptr(variant, count, wpb) : nullptr)
+                                 : (wpb == 4 ? render_ptr(variant, cull, count) : nullptr);
     if (!fn) return hipErrorInvalidValue;
     const size_t lds = (size_t)p.lds_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};
-    return hipLaunchKernel(fn, dim3(grid), dim3(256), args, lds, stream);
+    return hipLaunchKernel(fn, dim3(grid), dim3(64u * (uint32_t)wpb), args, lds, stream);
+}
+
+// workgroups per CU and static LDS of the deep kernel with wpb waves per workgroup
+hipError_t deep_occupancy(int variant, int wpb, size_t lds, int *blocks_per_cu, size_t *static_lds)
+{
+    const void *fn = render_deep_ptr(variant, false, wpb);
+    if (!fn) return hipErrorInvalidValue;
+    hipFuncAttributes a{};
+    hipError_t e = hipFuncGetAttributes(&a, fn);
+    if (e != hipSuccess) return e;
+    *static_lds = a.sharedSizeBytes;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64 * wpb, lds);
 }
 
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds)

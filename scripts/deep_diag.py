@@ -19,8 +19,10 @@ from bench import CONFIGS  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--options", nargs="*", default=[""])
+ap.add_argument("--depth", type=int, default=0, help="override the config's max depth")
 a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
+depth = a.depth or depth
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H)
 p = rt.make_params(W, H, spp, depth, 1234)
@@ -48,6 +50,9 @@ for text in a.options:
            "cycles_per_wave_iter": round(cyc / max(1, c["wave_iters"]), 1),
            "events": {k: int(v) for k, v in ev.items() if v},
            "busy_wave_exit_us": {f"p{int(f * 100)}": q(ends, f) for f in (0.0, 0.1, 0.5, 0.9, 0.99, 1.0)},
+           "busy_wave_dry_us": {f"p{int(f * 100)}": q(sorted(r[0] - t0 for r in busy), f) for f in (0.0, 0.1, 0.5, 0.9, 1.0)},
+           "idle_wave_exit_us": {f"p{int(f * 100)}": q(sorted(r[1] - t0 for r in tl if r[2] == 0), f)
+                                 for f in (0.0, 0.1, 0.5, 0.9, 1.0)},
            "iters_per_busy_wave": {f"p{int(f * 100)}": (sorted(r[2] for r in busy)[min(len(busy) - 1, int(f * len(busy)))] if busy else None)
                                    for f in (0.0, 0.5, 0.9, 1.0)}}
     print(json.dumps(res), flush=True)

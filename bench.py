@@ -192,10 +192,12 @@ def lib_sha256():
 
 
 # the timed kernels: rt::render_kernel<0, 7, false, false> (main launch) and
-# rt::render_deep_kernel<0, false, false> (the deep launch of a split pass)
+# rt::render_deep_kernel<0, false, false, 4 | 8> (the deep launch of a split pass: 4-wave groups
+# beside other renders, 8-wave groups for a lone pass)
 TIMED_KERNEL = ("_ZN2rt13render_kernelILi0ELi7ELb0ELb0EEEvNS_7KParamsE",
-                "_ZN2rt18render_deep_kernelILi0ELb0ELb0EEEvNS_7KParamsE")
-TIMED_KERNEL_NAMES = "render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false>"
+                "_ZN2rt18render_deep_kernelILi0ELb0ELb0ELi4EEEvNS_7KParamsE",
+                "_ZN2rt18render_deep_kernelILi0ELb0ELb0ELi8EEEvNS_7KParamsE")
+TIMED_KERNEL_NAMES = "render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false, 4|8>"
 
 
 def hashlib_sha256(b):

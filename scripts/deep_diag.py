@@ -20,9 +20,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--options", nargs="*", default=[""])
 ap.add_argument("--depth", type=int, default=0, help="override the config's max depth")
+ap.add_argument("--spp", type=int, default=0, help="override the config's samples per pixel")
 a = ap.parse_args()
 scene, W, H, spp, depth = CONFIGS[a.config]
 depth = a.depth or depth
+spp = a.spp or spp
 arrays = rt.huge_scene_arrays(1234) if scene == "huge" else rt.simple_scene_arrays()
 cam = rt.Camera.default(W, H)
 p = rt.make_params(W, H, spp, depth, 1234)

@@ -817,6 +817,10 @@ __device__ __forceinline__ float4 dielectric_record(const KP &P, const float4 *b
 #endif
 template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_PER_SIMD;
+// the lone deep kernel's occupancy bound (waves per SIMD; 6: 3 workgroups of 8 waves per CU)
+#ifndef RT_DEEP_WIDE_WAVES
+#define RT_DEEP_WIDE_WAVES 6
+#endif
 // The render loop; DEEP: the deep launch of a split pass (KParams::deep_mode),
 // whose items are queued paths (no sample starts, no lens draws, no split) — its own
 // instantiation, render_deep_kernel, so neither launch carries the other's code.
@@ -1448,7 +1452,7 @@ __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kerne
 // the deep launch of a split pass (culled scenes only); WPB = 8: the lone deep launch with the
 // shading records in LDS, whose workgroups per CU the LDS bounds
 template <int V, bool STATS, bool COUNT, int WPB>
-__global__ __launch_bounds__(64 * WPB, (WPB == 8 && !STATS ? 6 : kMinWaves<V, 7, STATS>)) void render_deep_kernel(const KParams p)
+__global__ __launch_bounds__(64 * WPB, (WPB == 8 && !STATS ? RT_DEEP_WIDE_WAVES : kMinWaves<V, 7, STATS>)) void render_deep_kernel(const KParams p)
 {
     render_body<V, 7, STATS, COUNT, true, WPB>(p);
 }

@@ -144,5 +144,15 @@ int main()
     run(ub::bounce<0>, "empty loop");
     run(ub::bounce<4>, "empty loop + 3 kernarg re-reads");
     run(ub::bounce<7>, "full bounce + 3 kernarg re-reads");
+    // the same bounce on 1024 waves at once (one per SIMD), as in a deep launch
+    {
+        unsigned long long c = 0;
+        for (int rep = 0; rep < 3; ++rep) {
+            hipLaunchKernelGGL(ub::bounce<3>, dim3(1024), dim3(64), 0, 0, up);
+            (void)hipDeviceSynchronize();
+            (void)hipMemcpy(&c, dc, sizeof(c), hipMemcpyDeviceToHost);
+        }
+        std::printf("%-28s %8.0f cycles per iteration (1024 waves, wave 0 of block 0)\n", "full bounce, 1024 waves", (double)c / iters);
+    }
     return 0;
 }

@@ -435,7 +435,11 @@ def main():
         frame_r = torch.empty((rows * rehearse, W, 3), dtype=torch.float32, device=dev)
 
     def out_frame():
-        """rank 0's output of a step: the gathered frame (N > 1) or its own tile."""
+        """rank 0's output of a step: the gathered frame (N > 1), the stood-in gathered frame of a
+        rehearsal with --rehearse-gather (so its frame wall clock ends with the whole frame's copy
+        to the host), or its own tile."""
+        if rehearse and args.rehearse_gather:
+            return frame_r
         return gather.frame if (world > 1 and not rehearse) else (tile8 if rgb8 else tile)
 
     # the reference's entry returns the frame in host memory (cuda_impl.cu:449-452): the frame
@@ -478,7 +482,8 @@ def main():
         elapsed = time.perf_counter() - t0
         spans = ds.kernel_times(steps)  # HIP-event spans of the timed frames' render launches
         if check_parity and rank == 0:
-            frame = out_frame().cpu().numpy()
+            # a rehearsal checks its own rows (the stood-in gather buffer holds copies of them)
+            frame = (tile8 if rgb8 else tile).cpu().numpy() if rehearse else out_frame().cpu().numpy()
             off, stride = (0, 1) if not rehearse else (params.row_offset, params.row_stride)
             parity.update(parity_record(frame, args.config, W, H, off, stride, args.seed, args.camera,
                                         args.variant, args.output))
@@ -644,6 +649,21 @@ def main():
                                 + ("gather's device copies stood in on the caller stream" if args.rehearse_gather
                                    else "no gather") + "; value = "
                                 f"this rank's Mrays/s, x{rehearse} for the ideal {rehearse}-GPU job")
+            if args.rehearse_gather:
+                # the N-GPU frame as one rank sees it, REHEARSED ON ONE GPU, NOT MEASURED: its share's
+                # lone frame with the gather's device work stood in (the N-1 peer tiles copied into
+                # the gather buffer, the de-interleave) and the whole frame copied to host memory,
+                # plus the peers' tiles over xGMI, which one GPU cannot run: each peer sends its
+                # tile on its own link at once, estimated at 50 GB/s per link
+                tile_bytes = rows * W * (3 if rgb8 else 12)
+                xgmi_ms = tile_bytes / 50e9 * 1e3
+                rec["rehearsal_projection"] = {
+                    "n_gpus": rehearse, "share_period_ms": r3(main_m["ms_per_step"]),
+                    "share_frame_wall_ms": r3(main_m["frame_wall_ms"]),
+                    "xgmi_tile_bytes": tile_bytes, "xgmi_estimate_ms": round(xgmi_ms, 4),
+                    "projected_frame_wall_ms": r3(main_m["frame_wall_ms"] + xgmi_ms),
+                    "note": "rehearsed on one GPU, not measured: rank 0's rows alone, the gather's device copies "
+                            "and the full-frame D2H copy stood in; xGMI transfer time estimated"}
         if world == 1 and not args.no_cpu_baseline and not rehearse:
             rec["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], args.camera, args.seed, args.cpu_rows,
                                                args.cpu_threads)

@@ -171,9 +171,13 @@ enum rt_diag {
     RT_DIAG_STATS = 1u << 6,           /* the instrumented kernel (rt_scene_debug_*)           */
     RT_DIAG_STATS_DEEP_ONLY = 1u << 7, /* with STATS: count the deep launch alone             */
     RT_DIAG_VERBOSE = 1u << 8,         /* print every launch's plan to stderr                 */
-    RT_DIAG_STANDIN_TRANSPORT = 1u << 9 /* rt_multi with every rank on one device: the RCCL
+    RT_DIAG_STANDIN_TRANSPORT = 1u << 9, /* rt_multi with every rank on one device: the RCCL
                                           gather code path, RCCL replaced by stream-ordered
                                           device copies (tests of that path on one GPU)       */
+    RT_DIAG_UNBOUNDED_NB = 1u << 10,    /* with STATS: the walk shortcut's neighbour slots formed
+                                          without the lane's own bound (the pre-fd383c3 form),
+                                          for the bounds check to report (rt_scene_debug_counters) */
+    RT_DIAG_NO_PAIRS = 1u << 11         /* one sample per item and slot (no sample pairs)       */
 };
 int rt_options_default(rt_options *out);
 /* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,
@@ -280,7 +284,9 @@ typedef struct rt_scene_usage {
     uint32_t pass_samples;     /* samples per pass of the last render                        */
     uint32_t static_lds_bytes; /* the culled render kernel's static LDS per workgroup        */
     uint32_t max_lds_bytes;    /* the device's LDS per workgroup                              */
-    uint32_t reserved;
+    uint32_t deep_launch;      /* the last render's last deep-path launch: waves per workgroup
+                                  (4: beside other renders; 8: a lone pass, shading records in
+                                  LDS) | 16 when it dealt its chunks statically; 0 = none      */
 } rt_scene_usage;
 int rt_scene_usage_get(const rt_scene *scene, rt_scene_usage *out);
 /* Spans (ms, HIP events) of the render kernels of the most recent calls of
@@ -296,12 +302,17 @@ int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n)
  * [4] wave / [5] lane root evaluations, [6] segments, [7] wave-level blocks of 8 cluster
  * members executed, [8..12] shader-clock cycles summed over waves per loop region
  * (refill, sample start + rejection loop, closest hit, shading, fold), [14] ~(earliest wave
- * start, 100 MHz clock). Copies them out; reset zeroes.                                */
+ * start, 100 MHz clock), [15] the bounds check's first violation, code << 32 | index
+ * (rt_device.h BoundsCode; 0 = none). Copies them out; reset zeroes. Returns RT_ERR_DEVICE
+ * (the message names the index) when [15] is set: the instrumented kernel checks every
+ * lane-computed index into the scene, the sample slots and the deep queue before using it. */
 int rt_scene_debug_counters(rt_scene *scene, uint64_t out[16], int reset);
 /* Diagnostics: per-wave records of the last instrumented render launch, out[4w .. 4w+3] for
  * wave w of the grid = {time the wave found every queue dry, exit} (100 MHz realtime
- * clock), loop iterations, and (hardware CU id << 32 | iterations after dry << 16 | refill
- * rounds); at most max_waves records, *n = records written (0 without RT_DIAG_STATS).      */
+ * clock), (shader-clock cycles in the loop << 32 | refill rounds << 16 | loop iterations),
+ * and (hardware CU id << 48 | iterations after dry << 32 | low 32 bits of the wave's start on
+ * the realtime clock); at most max_waves records, *n = records written (0 without
+ * RT_DIAG_STATS).                                                                            */
 int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, uint32_t *n);
 /* Diagnostics: with RT_DIAG_STATS, how often each block of the render loop ran, counted once
  * per wave per execution, summed over the instrumented launches since the last reset: [0] loop
@@ -309,7 +320,10 @@ int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, 
  * [5] scatters done, [6] root-box passes, [7] level-2 boxes walked, [8] level-2 boxes passed,
  * [9] clusters requested, [10] transposed member tests, [11] their rounds, [12] their far-root
  * passes, [13] per-lane member tests, [14] sky, [15] hit shading, [16] lambert, [17] unit
- * direction (metal/dielectric), [18] dielectric, [19] sample stores, [20] metal absorptions.   */
+ * direction (metal/dielectric), [18] dielectric, [19] sample stores, [20] metal absorptions,
+ * [21] live lanes summed over iterations, [22] iterations after the item queues ran dry, [23]
+ * live lanes summed over those, [24] lanes that skipped the walk (shortcut), [25] iterations
+ * whose walk no lane needed.                                        */
 int rt_scene_debug_events(rt_scene *scene, uint64_t out[32], int reset);
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,

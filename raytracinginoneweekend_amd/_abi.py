@@ -71,14 +71,14 @@ class RtSceneUsage(C.Structure):
     _fields_ = [
         ("device_bytes", C.c_uint64), ("workspace_bytes", C.c_uint64), ("render_streams", C.c_uint32),
         ("workspaces", C.c_uint32), ("pass_samples", C.c_uint32), ("static_lds_bytes", C.c_uint32),
-        ("max_lds_bytes", C.c_uint32), ("reserved", C.c_uint32),
+        ("max_lds_bytes", C.c_uint32), ("deep_launch", C.c_uint32),
     ]
 
 
 RT_DIAG = {
     "ieee_roots": 1 << 0, "no_shortcut": 1 << 1, "no_neighbours": 1 << 2, "no_root_box": 1 << 3,
     "shade_lds": 1 << 4, "shade_global": 1 << 5, "stats": 1 << 6, "stats_deep_only": 1 << 7, "verbose": 1 << 8,
-    "standin_transport": 1 << 9,
+    "standin_transport": 1 << 9, "unbounded_nb": 1 << 10, "no_pairs": 1 << 11,
 }
 
 

@@ -34,11 +34,33 @@ struct FrameConsts {
     uint32_t tile_lw;  // log2 of the tile width (3..6): tiles of 2^lw x 64/2^lw pixels
     float rW, rH;       // RN(1 / width), RN(1 / height)
     uint32_t div_fast;  // bit 0 / 1: x / width, x / height by rW / rH + one FMA correction is exact
+    uint32_t n_pairs;   // sample pairs per pixel in this pass (KParams::n_pair_items / n_pixels)
 };
+
+// Sample pairs. The reference sums a pixel's samples as ((c0+c1)+(c2+c3)) per
+// block of 4 (libstdc++ reduce): the pair sums c0+c1 and c2+c3 are all the accumulation needs of a
+// block. A pass's full blocks are dealt as pair items — one lane traces samples 2j and 2j+1 of a
+// pixel one after the other, parking c_2j in its LDS words, and stores RN(c_2j + c_2j+1) to
+// the pair's slot (12 B per two samples); the pass's tail samples (spp % 4) stay single items.
+// A main-launch lane keeps one word for its item: the item's slot (= its item index: pair items
+// first, then the tail's single samples) in the low bits, these flags above; the pixel and the
+// sample are re-derived from it where a sample starts.
+constexpr uint32_t kItSlot = (1u << 29) - 1u;
+constexpr uint32_t kItSecond = 1u << 31;     // tracing the pair's second sample
+constexpr uint32_t kItFirstDeep = 1u << 30;  // the pair's first sample went to the deep queue
+constexpr uint32_t kItRestart = 1u << 29;    // start the pair's second sample next iteration
+// the deep queue's pair link of a path (DeepQueue::link): its role in the top two bits, the
+// partner path's queue index below (both samples of a pair queued)
+constexpr uint32_t kRoleSingle = 0u;       // a single sample: its colour is the slot's
+constexpr uint32_t kRolePartnerDone = 1u;  // the partner's colour is in the pair's slot: add to it
+constexpr uint32_t kRoleBothFirst = 2u;    // both samples queued; this is the first
+constexpr uint32_t kRoleBothSecond = 3u;   // both samples queued; this is the second
+constexpr uint32_t kLinkIndex = 0x3fffffffu;
 
 // The deep queue of one workspace (structure of arrays, 8 regions of rcap paths): f =
 // [9][8 rcap] floats {o.xyz, d.xyz, attenuation.xyz} of the next segment, the data-stream state,
-// the sample's slot index and the path's hint sphere (52 B per path). Region r is appended to by workgroups r mod 8; its counters sit in
+// the sample's slot index, the path's hint sphere, its pair link and the both-deep arrival word
+// (60 B per path). Region r is appended to by workgroups r mod 8; its counters sit in
 // the workspace's queue-counter block, line r: word kDeepCount = paths appended (may exceed
 // rcap: lanes past it keep their path), word kDeepDeal = the deep launch's dealing counter;
 // they are reset with the queue counters.
@@ -48,6 +70,8 @@ struct DeepQueue {
     uint32_t *slot;
     uint32_t *hid;           // the dielectric sphere the path last hit (its hint), ~0 = none
     uint32_t *ctr;           // the workspace's queue-counter block (8 x kQueueStride words)
+    uint32_t *link;          // pair link (role << 30 | partner's index, kRole*)
+    uint32_t *meet;          // both-deep pairs: arrivals at the first's index (0 between passes)
     uint32_t rcap;
     uint8_t *px;             // [n_pixels] 1: some sample of the pixel went to the queue (cleared by
                              // the accumulation that reads it)
@@ -69,6 +93,8 @@ struct KParams {
     uint32_t tile_lw;                       // log2 of the tile width (3: 8x8, 4: 16x4, 5: 32x2, 6: 64x1)
     uint32_t sample_begin, sample_end;      // this launch's samples
     uint32_t n_items;
+    uint32_t n_pair_items;   // items [0, n_pair_items) are sample pairs (FrameConsts::n_pairs x n_pixels),
+                             // the rest single tail samples; the slot of item I is slot I either way
     uint32_t n_blocks;       // guided dealing: ceil(n_items / 64) blocks, 1/8 per queue
     float guided_l2b;        // log2(beta) < 0 of the guided dealing (rt_kernel.hip refill)
     // scene
@@ -104,10 +130,24 @@ struct KParams {
     uint32_t deep_mode;      // the deep launch: the split depth (its paths resume there); 0 otherwise
     uint32_t deep_prio;      // the deep launch's waves at the highest issue priority (s_setprio 3)
     uint32_t deep_static;    // the deep launch deals chunk j to wave j mod (waves of the grid), no atomics
+    // instrumented kernel only (V_STATS_LDS): hint_candidate's neighbour slots formed without the
+    // lane's own bound (the form before fd383c3), so that the bounds check sees stale words
+    uint32_t diag_unbounded_nb;
+};
+// V_STATS_LDS: every lane-computed index into the scene blob, the slots and the deep queue is
+// checked against its bound before use; the first violation is recorded in dbg[kDbgError] as
+// code << 32 | index (and the access is made at index 0 instead), rt_scene_debug_counters turns
+// it into RT_ERR_DEVICE
+constexpr uint32_t kDbgError = 15;
+enum BoundsCode : uint32_t {
+    BC_NONE = 0, BC_HINT_NB = 1, BC_SHADE = 2, BC_SLOT = 3, BC_DEEP_APPEND = 4, BC_DEEP_ITEM = 5,
+    BC_DEEP_HINT = 6, BC_MEMBERS = 7, BC_DEEP_PX = 8
 };
 
 struct KAccum {
-    const float *slots;      // [n_samples][n_pixels][3], first sample a multiple of 4
+    const float *slots;      // [n_samples][n_pixels][3], first sample a multiple of 4; paired: the
+                             // pass's 2 n_blocks pair sums, then its n_samples - 4 n_blocks tail samples
+    uint32_t paired;
     float *acc;              // [n_pixels][3] running sum between passes
     float *out;              // final f32 RGB
     uint8_t *out_u8;         // optional gamma/u8 output (same layout)

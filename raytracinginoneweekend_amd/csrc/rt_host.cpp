@@ -142,6 +142,9 @@ struct rt_scene {
     // accumulation clears the flags it set, so only a larger pixel count needs a memset)
     void *deep[kMaxWs] = {};
     size_t deep_bytes[kMaxWs] = {}, deep_clean[kMaxWs] = {};
+    // where the pair-arrival words of the queue of workspace w lay in its last layout (the
+    // arrays' offsets follow the pixel count and the region capacity): zeroed again when moved
+    size_t deep_meet_at[kMaxWs] = {};
     // deep-queue overflow reports (pinned host memory written by accumulate_kernel, one word per
     // workspace) and the camera keys they named, with the call that last reported each: renders
     // with such a camera are not split for kDeepOffCalls calls; at most kDeepOffKeys keys (LRU)
@@ -177,9 +180,11 @@ struct rt_scene {
     unsigned long long *dbg = nullptr;  // diagnostic counters (RT_DIAG_STATS)
     uint32_t dbg_waves = 0;             // waves of the last instrumented launch
     size_t max_lds = 0;
-    size_t static_lds = 0;  // the culled render kernel's static LDS (hipFuncGetAttributes)
+    // static LDS of the render kernel per traversal, [0] brute force, [1] culled (per-wave
+    // transposed-test records and per-lane arrays; hipFuncGetAttributes)
+    size_t static_lds[2] = {0, 0};
     // the last render's cut (rt_scene_usage_get)
-    uint32_t used_streams = 0, used_ws = 0, used_pass = 0;
+    uint32_t used_streams = 0, used_ws = 0, used_pass = 0, used_deep = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
     static constexpr uint32_t kRing = 256;
     std::vector<hipEvent_t> ev_begin, ev_end;
@@ -259,6 +264,7 @@ void fill_frame_consts(rt::KParams &k)
     f.rW = 1.f / f.fW;
     f.rH = 1.f / f.fH;
     f.div_fast = (exact_by_reciprocal(f.fW) ? 1u : 0u) | (exact_by_reciprocal(f.fH) ? 2u : 0u);
+    f.n_pairs = k.n_pair_items / k.n_pixels;
 }
 
 bool camera_in_fast_range(const rt_camera &c)
@@ -278,14 +284,14 @@ bool camera_in_fast_range(const rt_camera &c)
 // (a frame stream) are split at any size: the unsplit drain costs issue (the 8-way share ran
 // 42% more VALU instructions per sample than the full frame) and the deep launches run beside
 // the other frames (8-way share, 7 streams: 0.50-0.51 ms per frame vs 0.58-0.59 unsplit).
-uint32_t deep_region_cap(uint64_t n_items)
+uint32_t deep_region_cap(uint64_t n_samples)
 {
-    return static_cast<uint32_t>(std::max<uint64_t>(512u, n_items / 1024u));
+    return static_cast<uint32_t>(std::max<uint64_t>(512u, n_samples / 1024u));
 }
 size_t deep_px_bytes(uint64_t n_pixels) { return (n_pixels + 255u) & ~static_cast<size_t>(255u); }
-size_t deep_queue_bytes(uint64_t n_pixels, uint64_t n_items)
+size_t deep_queue_bytes(uint64_t n_pixels, uint64_t n_samples)
 {
-    return deep_px_bytes(n_pixels) + static_cast<size_t>(8u) * deep_region_cap(n_items) * 52u;
+    return deep_px_bytes(n_pixels) + static_cast<size_t>(8u) * deep_region_cap(n_samples) * 60u;
 }
 // a nonzero key of the camera basis and the depth limit (FNV-1a over their bytes)
 unsigned long long camera_key(const rt_camera &c, uint32_t max_depth)
@@ -513,7 +519,8 @@ int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_ma
         }
     }
     if (rc == RT_OK) {
-        hipError_t e = rt::static_lds_render(rt::V_EXACT_LDS, 7, &sc->static_lds);
+        hipError_t e = rt::static_lds_render(rt::V_EXACT_LDS, 0, &sc->static_lds[0]);
+        if (e == hipSuccess) e = rt::static_lds_render(rt::V_EXACT_LDS, 7, &sc->static_lds[1]);
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(e));
     }
     for (uint32_t i = 0; rc == RT_OK && i < rt_scene::kRing; ++i) {
@@ -551,6 +558,7 @@ int free_workspaces(rt_scene *sc)
         sc->slots[w] = nullptr;
         RT_HIP(drop(sc->deep[w], sc->deep_bytes[w]));
         sc->deep_clean[w] = 0;
+        sc->deep_meet_at[w] = 0;
     }
     void *ap = sc->acc;
     RT_HIP(drop(ap, sc->acc_bytes));
@@ -635,7 +643,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
 
     // Variant: exact (bit-exact) or fast (tolerance); clustered culling unless brute force is
     // asked for; the scalar-cache A/B variant is brute force only. Each needs its blob in LDS
-    // next to the kernel's static LDS (sc->static_lds, the culled kernel's: the largest).
+    // next to the static LDS of the kernel of its traversal (sc->static_lds[culled]).
     const rt_options &O = sc->opt;
     int variant = (P.flags & RT_FLAG_FAST_MATH) ? rt::V_FAST_LDS : rt::V_EXACT_LDS;
     bool cull = !(P.flags & RT_FLAG_BRUTE_FORCE) && sc->n_clusters[1] > 0;
@@ -643,7 +651,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     if (wave && (P.flags & (RT_FLAG_FAST_MATH | RT_FLAG_SCALAR_SCENE)))
         return fail(RT_ERR_UNSUPPORTED, "rt_render_device: the wavefront variant is the exact kernel only");
     if (P.flags & RT_FLAG_SCALAR_SCENE) { variant = rt::V_EXACT_SCALAR; cull = false; }
-    if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->shade_offset[cull]) * 16u + sc->static_lds > sc->max_lds) {
+    if (variant != rt::V_EXACT_SCALAR && static_cast<size_t>(sc->shade_offset[cull]) * 16u + sc->static_lds[cull] > sc->max_lds) {
         if (variant == rt::V_FAST_LDS || cull) return fail(RT_ERR_UNSUPPORTED, "rt_render_device: scene too large for LDS");
         variant = rt::V_EXACT_SCALAR;
     }
@@ -671,6 +679,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     k.use_root = (O.diag & RT_DIAG_NO_ROOT_BOX) ? 0u : 1u;
     k.iso = (O.diag & RT_DIAG_NO_SHORTCUT) ? 0u : 1u;
     k.transpose_max = O.transpose_max;
+    k.diag_unbounded_nb = (O.diag & RT_DIAG_UNBOUNDED_NB) ? 1u : 0u;
     k.fast_roots = sc->in_fast_range && camera_in_fast_range(*camera) && !(O.diag & RT_DIAG_IEEE_ROOTS) ? 1u : 0u;
     k.shade_offset = sc->shade_offset[b];
     // the shading records (the blob's tail) join the geometry in LDS unless that costs
@@ -688,7 +697,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     int occ_geo = 0, occ_all = 0;
     if (int rc = occ_for(0, &occ_geo); rc) return rc;
     if (int rc = occ_for(1, &occ_all); rc) return rc;
-    const bool shade_fits = static_cast<size_t>(k.blob_units) * 16u + sc->static_lds <= sc->max_lds;
+    const bool shade_fits = static_cast<size_t>(k.blob_units) * 16u + sc->static_lds[cull] <= sc->max_lds;
     k.shade_lds = variant != rt::V_EXACT_SCALAR && shade_fits &&
                   ((O.diag & RT_DIAG_SHADE_LDS) ? true : (O.diag & RT_DIAG_SHADE_GLOBAL) ? false : occ_all >= occ_geo);
     k.lds_units = variant == rt::V_EXACT_SCALAR ? 0u : (k.shade_lds ? k.blob_units : k.shade_offset);
@@ -732,6 +741,25 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // per frame in that order (7 workspaces, 52-sample passes) vs 2.79 shrinking the passes first
     // (14 workspaces, 24-sample passes), 2.56 uncapped (19.1 GiB; profiles/r04).
     const uint64_t per_sample = n_pixels * 12ull;
+    // Sample pairs: a pass's full blocks of 4 samples take two pair slots each,
+    // its tail samples one. Passes issued while other renders run take pairs (half the slot
+    // memory and traffic, the same frame period); a pass issued alone (a lone frame) takes single
+    // samples, whose shorter items end the launch sooner (config 3: 3.23-3.26 vs 3.38-3.45 ms),
+    // in a workspace of its own beside the ring. The wavefront variant stores single samples.
+    const bool pairs_ok = !wave && !(O.diag & RT_DIAG_NO_PAIRS);
+    const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
+    auto slot_rows = [&](uint64_t a, uint64_t b, bool pr) -> uint64_t {  // samples [a, b), a a multiple of 4
+        const uint64_t nb = (std::min<uint64_t>(b, full_blocks_end) - std::min<uint64_t>(a, full_blocks_end)) / 4u;
+        return pr ? (b - a) - 2u * nb : (b - a);
+    };
+    // the most slot rows of a pass of at most sp samples: a pass holding the tail (single samples)
+    // can take more rows than a full one (pairs)
+    auto max_rows = [&](uint64_t sp, bool pr) {
+        uint64_t m = 0;
+        for (uint64_t a = 0; a < P.spp; a += sp) m = std::max(m, slot_rows(a, std::min<uint64_t>(P.spp, a + sp), pr));
+        return m;
+    };
+    auto ws_bytes = [&](uint64_t sp, bool pr) { return per_sample * max_rows(sp, pr); };
     const uint64_t items_cap = ((1ull << 31) - 8192) / n_pixels;  // items fit 31 bits
     uint64_t spp_full = std::min<uint64_t>({P.spp, O.max_pass_bytes / per_sample, items_cap});
     if (spp_full < P.spp) spp_full &= ~3ull;
@@ -742,10 +770,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         return static_cast<uint32_t>(std::min<uint64_t>(n_pixels * std::min<uint64_t>(sp, P.spp), O.wave_queue_rays));
     };
     auto n_ws_of = [](uint32_t streams, uint32_t wsps) { return streams > 1 ? streams * wsps : 1u; };
+    // the ring's workspaces (pairs when there is a ring) and the lone passes' own one (singles)
     auto footprint = [&](uint32_t streams, uint32_t wsps, uint64_t sp) -> uint64_t {
         const uint64_t spe = std::min<uint64_t>(sp, P.spp);
-        uint64_t t = static_cast<uint64_t>(n_ws_of(streams, wsps)) *
-                     (per_sample * spe + (may_split ? deep_queue_bytes(n_pixels, n_pixels * spe) : 0u));
+        const bool ring_pairs = pairs_ok && streams > 1;
+        const uint64_t dq = may_split ? deep_queue_bytes(n_pixels, n_pixels * spe) : 0u;
+        uint64_t t = static_cast<uint64_t>(n_ws_of(streams, wsps)) * (ws_bytes(spe, ring_pairs) + dq);
+        if (ring_pairs) t += ws_bytes(spe, false) + dq;
         if (sp < P.spp) t += per_sample;  // the multi-pass sums
         if (wave) t += 2ull * wave_cap(sp) * 52u + 512u;
         return t;
@@ -773,13 +804,17 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     const bool pipe = bufs > 1;
     const uint32_t n_ws = n_ws_of(bufs, wsps);
     const uint64_t spe = std::min<uint64_t>(spp_pass, P.spp);
+    const bool ring_pairs = pairs_ok && pipe;
+    const uint32_t lone_ws = ring_pairs ? n_ws : kMaxWs;  // the lone passes' workspace (singles), if any
+    auto ws_size = [&](uint32_t w) { return ws_bytes(spe, ring_pairs && w != lone_ws); };
     // under a cap, workspaces left larger (or more numerous) by earlier frames are re-cut once
     if (O.max_workspace_bytes) {
         uint64_t after = 0;
         for (uint32_t w = 0; w < kMaxWs; ++w) {
-            after += w < n_ws ? std::max<uint64_t>(sc->slots_bytes[w], per_sample * spe) : sc->slots_bytes[w];
-            after += w < n_ws && may_split ? std::max<uint64_t>(sc->deep_bytes[w], deep_queue_bytes(n_pixels, n_pixels * spe))
-                                           : sc->deep_bytes[w];
+            const bool used = w < n_ws || w == lone_ws;
+            after += used ? std::max<uint64_t>(sc->slots_bytes[w], ws_size(w)) : sc->slots_bytes[w];
+            after += used && may_split ? std::max<uint64_t>(sc->deep_bytes[w], deep_queue_bytes(n_pixels, n_pixels * spe))
+                                       : sc->deep_bytes[w];
         }
         after += spp_pass < P.spp ? std::max<uint64_t>(sc->acc_bytes, per_sample) : sc->acc_bytes;
         after += wave ? std::max<uint64_t>(sc->wq_bytes, 2ull * wave_cap(spp_pass) * 52u + 512u) : sc->wq_bytes;
@@ -787,12 +822,15 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             if (int rc = free_workspaces(sc); rc) return rc;
     }
     sc->used_streams = bufs;
-    sc->used_ws = n_ws;
+    sc->used_ws = n_ws + (ring_pairs ? 1u : 0u);
     sc->used_pass = static_cast<uint32_t>(spe);
+    sc->used_deep = 0;
     if (spp_pass < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
     for (uint32_t w = 0; w < n_ws; ++w)
-        if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], per_sample * spe); rc) return rc;
+        if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], ws_size(w)); rc) return rc;
+    if (ring_pairs)
+        if (int rc = ensure((void **)&sc->slots[lone_ws], &sc->slots_bytes[lone_ws], ws_size(lone_ws)); rc) return rc;
     // wavefront variant: two ray queues of cap rays (52 B each) and their counters
     uint32_t wcap = 0;
     rt::RayQueue wqa{}, wqb{};
@@ -822,16 +860,22 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
 
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
-    const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     for (uint32_t s0 = 0; s0 < P.spp; s0 += static_cast<uint32_t>(spp_pass)) {
         const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
-        // every pass takes the next workspace and stream: pass p + 1's render overlaps pass
-        // p's drain and accumulation, within a frame and across frames
-        const uint32_t wb = pipe ? sc->next_buf % n_ws : 0u;
-        sc->next_buf = wb + 1u;
-        hipStream_t xst = pipe ? sc->xs[wb % bufs] : st;
         // another render still running? (then this one takes a partial grid, grid_wg_per_cu)
         const bool in_flight = pipe && sc->last_ws >= 0 && hipEventQuery(sc->ev_done[sc->last_ws]) == hipErrorNotReady;
+        // every pass takes the next workspace and stream: pass p + 1's render overlaps pass
+        // p's drain and accumulation, within a frame and across frames; a pass issued alone takes
+        // the lone passes' workspace (single samples) when the ring holds pairs
+        const bool pass_pairs = ring_pairs && in_flight;
+        uint32_t wb = 0;
+        if (ring_pairs && !in_flight) {
+            wb = lone_ws;
+        } else if (pipe) {
+            wb = sc->next_buf % n_ws;
+            sc->next_buf = wb + 1u;
+        }
+        hipStream_t xst = pipe ? sc->xs[wb % bufs] : st;
         k.slots = sc->slots[wb];
         k.queue_ctr = sc->queue_ctr + wb * 8u * rt::kQueueStride;
         unsigned long long *seg_b = reinterpret_cast<unsigned long long *>(sc->queue_ctr + kSegWords) + 4u * wb;
@@ -845,10 +889,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         if (s0 == 0) RT_HIP(hipEventRecord(sc->ev_begin[ring], xst));
         k.sample_begin = s0;
         k.sample_end = s1;
+        k.n_pair_items = static_cast<uint32_t>(((s1 - s0) - slot_rows(s0, s1, pass_pairs)) * n_pixels);
         fill_frame_consts(k);
-        k.n_items = static_cast<uint32_t>(n_pixels * (s1 - s0));
+        // items: the pass's pair items and its single tail samples (one slot each)
+        const uint64_t n_samples = n_pixels * (s1 - s0);
+        k.n_items = static_cast<uint32_t>(n_pixels * slot_rows(s0, s1, pass_pairs));
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, k.n_items)) * sc->cu_count, (k.n_items + 255u) / 256u)));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, n_samples)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u, in_flight);
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
@@ -856,12 +903,21 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.deep_mode = 0;
         bool two_part = false;
         uint32_t stats_waves = 0;  // the instrumented build: waves of the launch the counters cover
-        if (may_split && (k.n_items >= O.deep_min_items || in_flight)) {
-            const uint32_t rcap = deep_region_cap(k.n_items), cap = 8u * rcap;
+        if (may_split && (n_samples >= O.deep_min_items || in_flight)) {
+            const uint32_t rcap = deep_region_cap(n_samples), cap = 8u * rcap;
             const size_t px_bytes = deep_px_bytes(n_pixels);
             void *had = sc->deep[wb];
-            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], deep_queue_bytes(n_pixels, k.n_items)); rc) return rc;
-            if (sc->deep[wb] != had) sc->deep_clean[wb] = 0;  // new memory
+            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], deep_queue_bytes(n_pixels, n_samples)); rc) return rc;
+            if (sc->deep[wb] != had) {  // new memory: no flag set, no pair arrival counted
+                sc->deep_clean[wb] = 0;
+                RT_HIP(hipMemsetAsync(sc->deep[wb], 0, sc->deep_bytes[wb], xst));
+            } else if (sc->deep_meet_at[wb] != px_bytes + static_cast<size_t>(cap) * 56u) {
+                // another layout: its arrival words lie where other arrays were (every pass that
+                // keeps the layout leaves them zero: the second arrival of a pair resets its word)
+                RT_HIP(hipMemsetAsync(static_cast<char *>(sc->deep[wb]) + px_bytes + static_cast<size_t>(cap) * 56u, 0,
+                                      static_cast<size_t>(cap) * 4u, xst));
+            }
+            sc->deep_meet_at[wb] = px_bytes + static_cast<size_t>(cap) * 56u;
             if (sc->deep_clean[wb] < px_bytes)  // flags over bytes a queue may have used
                 RT_HIP(hipMemsetAsync(sc->deep[wb], 0, px_bytes, xst));
             // every accumulation clears the flags its pass set, and the bytes past px_bytes are
@@ -874,6 +930,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             k.deep.rng = reinterpret_cast<uint64_t *>(base + static_cast<size_t>(cap) * 36u);
             k.deep.slot = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 44u);
             k.deep.hid = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 48u);
+            k.deep.link = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 52u);
+            k.deep.meet = reinterpret_cast<uint32_t *>(base + static_cast<size_t>(cap) * 56u);
             k.deep.ctr = k.queue_ctr;
             k.deep.rcap = rcap;
             k.deep_depth = deep_split;
@@ -941,10 +999,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                     int &ow = sc->occ_deep_wide[variant];
                     if (ow < 0) {
                         const size_t bytes = static_cast<size_t>(k.blob_units) * 16u;
-                        size_t st8 = 0;
-                        int o8 = 0;
+                        size_t st8 = 0, st4 = 0;
+                        int o8 = 0, o4 = 0;
                         RT_HIP(rt::deep_occupancy(variant, 8, bytes, &o8, &st8));
-                        ow = bytes + st8 <= sc->max_lds && o8 * 8 > occ_all * 4 ? o8 : 0;
+                        // against the 4-wave deep kernel it replaces, with the same blob in LDS
+                        // (the main kernel's occupancy stood in for it)
+                        RT_HIP(rt::deep_occupancy(variant, 4, bytes, &o4, &st4));
+                        ow = bytes + st8 <= sc->max_lds && o8 * 8 > o4 * 4 ? o8 : 0;
                     }
                     if (RT_DEEP_WIDE && ow > 0) {
                         wpb = 8;
@@ -958,6 +1019,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                     RT_HIP(hipMemsetAsync(sc->dbg + rt::kDbgEvBase, 0, rt::kDbgEvents * sizeof(unsigned long long), xst));
                 }
                 RT_HIP(rt::launch_render(variant, cull_mode, kd, dgrid, xst, wpb));
+                sc->used_deep = static_cast<uint32_t>(wpb) | (kd.deep_static ? 16u : 0u);
                 if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) stats_waves = dgrid * static_cast<uint32_t>(wpb);
             }
         }
@@ -975,6 +1037,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         a.n_pixels = k.n_pixels;
         a.n_samples = s1 - s0;
         a.n_blocks = (std::min(s1, full_blocks_end) - std::min(s0, full_blocks_end)) / 4u;
+        a.paired = k.n_pair_items ? 1u : 0u;
         a.first = s0 == 0;
         a.last = s1 == P.spp;
         a.spp = P.spp;
@@ -1111,7 +1174,8 @@ int rt_scene_usage_get(const rt_scene *sc, rt_scene_usage *out)
     u.render_streams = sc->used_streams;
     u.workspaces = sc->used_ws;
     u.pass_samples = sc->used_pass;
-    u.static_lds_bytes = static_cast<uint32_t>(sc->static_lds);
+    u.deep_launch = sc->used_deep;
+    u.static_lds_bytes = static_cast<uint32_t>(sc->static_lds[1]);
     u.max_lds_bytes = static_cast<uint32_t>(sc->max_lds);
     *out = u;
     return RT_OK;
@@ -1128,6 +1192,17 @@ int rt_scene_debug_counters(rt_scene *sc, uint64_t out[16], int reset)
     RT_HIP(hipDeviceSynchronize());
     RT_HIP(hipMemcpy(out, sc->dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     if (reset) RT_HIP(hipMemset(sc->dbg, 0, 16 * sizeof(uint64_t)));
+    // the instrumented kernel's bounds check (rt_device.h kDbgError): an index past its bound
+    if (const uint64_t e = out[rt::kDbgError]; e) {
+        static const char *const kWhat[] = {"?", "walk-shortcut neighbour slot", "shading record", "sample slot",
+                                            "deep-queue append", "deep-queue item", "deep-path hint sphere", "cluster members",
+                                            "deep pixel flag"};
+        const uint32_t code = static_cast<uint32_t>(e >> 32);
+        return fail(RT_ERR_DEVICE, std::string("rt_scene_debug_counters: bounds check: ") +
+                                       kWhat[code < sizeof(kWhat) / sizeof(kWhat[0]) ? code : 0] + " index " +
+                                       std::to_string(static_cast<uint32_t>(e)) + " past its bound (code " +
+                                       std::to_string(code) + ")");
+    }
     return RT_OK;
 }
 
@@ -1307,8 +1382,11 @@ ncclResult_t push(bool is_send, const void *src, void *dst, size_t count, ncclDa
 {
     comm *cc = reinterpret_cast<comm *>(c);
     if (!cc || !type_bytes(t) || peer < 0 || peer >= cc->n || peer == cc->rank) return ncclInvalidArgument;
+    // only grouped calls are emulated: a call outside a group is refused and leaves nothing behind
+    // for the next group to pair with
+    if (!g_depth) return ncclInvalidUsage;
     g_ops.push_back({is_send, src, dst, count * type_bytes(t), peer, cc, st});
-    return g_depth ? ncclSuccess : ncclInvalidUsage;  // only grouped calls are emulated
+    return ncclSuccess;
 }
 ncclResult_t send(const void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t c, hipStream_t st)
 {
@@ -1320,6 +1398,7 @@ ncclResult_t recv(void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_
 }
 ncclResult_t group_start()
 {
+    if (!g_depth) g_ops.clear();
     ++g_depth;
     return ncclSuccess;
 }

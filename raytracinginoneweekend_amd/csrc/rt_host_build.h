@@ -21,7 +21,7 @@ static_assert(kMaxSlotsBytes / 12 < (1ull << 32), "slot index width");
 // internal render streams for frames in flight (rt_options.render_streams, 2..kMaxBufs), and
 // workspaces: rt_options.workspaces_per_stream (1..2) per stream, at most kMaxWs
 constexpr uint32_t kMaxBufs = 8;
-constexpr uint32_t kMaxWs = 2 * kMaxBufs;
+constexpr uint32_t kMaxWs = 2 * kMaxBufs + 1;  // + the lone passes' own workspace (sample pairs, rt_host.cpp)
 
 rt_options library_defaults();
 int check_options(const rt_options &o);

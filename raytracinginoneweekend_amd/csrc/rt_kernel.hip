@@ -89,6 +89,19 @@ static_assert(EV_COUNT <= kDbgEvents, "event counters");
 __device__ __forceinline__ uint64_t ballot(bool x) { return __builtin_amdgcn_ballot_w64(x); }
 __device__ __forceinline__ uint32_t lanes(bool x) { return (uint32_t)__popcll(ballot(x)); }
 
+// Bounds check of the instrumented kernel (STATS; rt_device.h kDbgError): an index at or past its
+// bound is recorded (the first one wins) and replaced by 0, so the diagnostic never makes the
+// access it reports. The product kernels compile this to the index itself.
+template <bool STATS>
+__device__ __forceinline__ uint32_t checked(uint32_t i, uint32_t bound, uint32_t code, unsigned long long *dbg)
+{
+    if (STATS && i >= bound) {
+        atomicCAS(dbg + kDbgError, 0ull, ((unsigned long long)code << 32) | i);
+        return 0u;
+    }
+    return i;
+}
+
 // ---- RNG: PCG32 XSH-RR per (pixel, sample) stream; the increment is wave-uniform ---------
 constexpr uint64_t kPcgMul = 6364136223846793005ULL;
 __device__ __forceinline__ uint32_t pcg_out(uint64_t old)
@@ -538,10 +551,11 @@ __device__ __forceinline__ uint64_t min16_key(uint64_t k)
     const uint32_t im = min16_u32(tb == tm ? (uint32_t)k : 0xffffffffu);
     return ((uint64_t)tm << 32) | im;
 }
-// per-wave LDS of the transposed tests: the requesting rays by rank, and each ray's minimum
+// per-wave LDS of the transposed tests: the requesting rays by rank; a ray's minimum key comes
+// back in the last two words of its first record once its round is done (the round's rows read
+// their rays before any row writes a key, and later rounds read other rays)
 struct TransposeLds {
-    float4 ray[kTransposeMax][2];   // {o.x, o.y, o.z, a}, {d.x, d.y, d.z, refined 1/a}
-    uint64_t key[kTransposeMax];
+    float4 ray[kTransposeMax][2];   // {o.x, o.y, o.z | key lo, a | key hi}, {d.x, d.y, d.z, refined 1/a}
 };
 template <bool FAST, bool STATS>
 __device__ __forceinline__ void members_transposed(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
@@ -601,13 +615,17 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
             key = hit_key(t, sid);
         }
         key = min16_key(key);
-        if (k == 0u && r < m) tw->key[r] = key;
+        if (k == 0u && r < m) {
+            tw->ray[r][0].z = __uint_as_float((uint32_t)key);
+            tw->ray[r][0].w = __uint_as_float((uint32_t)(key >> 32));
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (req) {
-        const uint64_t kk = tw->key[rank];
+        const float4 q = tw->ray[rank][0];
+        const uint64_t kk = ((uint64_t)__float_as_uint(q.w) << 32) | __float_as_uint(q.z);
         if (kk < h.key) h.key = kk;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -687,10 +705,18 @@ __device__ __forceinline__ uint64_t sphere_key(bool want, float4 s, uint32_t id,
 // clustered sphere but the sphere's at most two neighbours (none: "isolated"), whose slots nbw
 // holds: the lane tests them here and needs no walk (`skip`; the always-tested spheres are still
 // tested). A ray trapped in a small glass ball takes this path for every bounce.
-template <bool FAST>
+//
+// The neighbour slots of a lane that does not test a neighbour are 0, not its word's: a lane's
+// word may be stale (left by an earlier path) or, before the lane's first dielectric hit, whatever
+// the LDS held — bounded by that lane's own `skip` since fd383c3. The instrumented kernel (STATS)
+// checks the slot against n_geo, starts every lane's word at 0x7fff7fff (slots past any blob), and
+// with `unbounded` (KParams::diag_unbounded_nb) forms it the old way, so the check fires
+// (tests/test_gpu_parity.py test_neighbour_slots_are_bounded).
+template <bool FAST, bool STATS>
 __device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t hid, uint32_t nbw,
                                                    const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
-                                                   f3 o, f3 d, const RayDiv &rd, uint32_t iso, bool &skip)
+                                                   f3 o, f3 d, const RayDiv &rd, uint32_t iso, bool &skip,
+                                                   uint32_t n_geo, uint32_t unbounded, unsigned long long *dbg)
 {
     skip = false;
     float t;
@@ -708,12 +734,14 @@ __device__ __forceinline__ uint64_t hint_candidate(bool hint, float4 s, uint32_t
         const uint32_t n0 = nbw & 0x7fffu, n1 = (nbw >> 15) & 0x7fffu;
         // (lanes that do not test a neighbour read slot 0: their word may be stale)
         if (ballot(skip && n0 != 0u)) {
-            const uint32_t g = skip && n0 ? n0 - 1u : 0u;
+            uint32_t g = (STATS && unbounded) ? (n0 ? n0 - 1u : 0u) : (skip && n0 ? n0 - 1u : 0u);
+            g = checked<STATS>(g, n_geo, BC_HINT_NB, dbg);
             const uint64_t k = sphere_key<FAST>(skip && n0 != 0u, geo[g], sidx[g], o, d, rd, t);
             if (k < key) key = k;
         }
         if (ballot(skip && n1 != 0u)) {
-            const uint32_t g = skip && n1 ? n1 - 1u : 0u;
+            uint32_t g = (STATS && unbounded) ? (n1 ? n1 - 1u : 0u) : (skip && n1 ? n1 - 1u : 0u);
+            g = checked<STATS>(g, n_geo, BC_HINT_NB, dbg);
             const uint64_t k = sphere_key<FAST>(skip && n1 != 0u, geo[g], sidx[g], o, d, rd, t);
             if (k < key) key = k;
         }
@@ -867,6 +895,10 @@ __device__ __forceinline__ void render_body(const KParams &p)
     __shared__ float4 lds_pn[64 * WPB];
     __shared__ uint32_t lds_hid[64 * WPB];
     __shared__ uint32_t lds_nb[64 * WPB];  // the dielectric sphere's shortcut word (hint_candidate)
+    // sample pairs, per lane (structure of arrays): the main launch parks a pair's first colour
+    // here while the lane traces the second (or, in word 0, the first's deep-queue index when it
+    // went to the queue); the deep launch keeps the path's own queue index in word 0
+    __shared__ float lds_park[3][64 * WPB];
     const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
     // the deep launch's waves issue ahead of other launches' waves (KParams::deep_prio): each of
@@ -883,7 +915,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
 
     // lane state: the lane's item is one sample (pixel enumeration index, sample of the pass)
     bool alive = false;
-    uint32_t pix = 0, ls = 0;
+    // the main launch: it = the item word (rt_device.h kIt*); the deep launch: pix = the path's
+    // slot, ls = its pair link
+    uint32_t it = 0, pix = 0, ls = 0;
     f3 o = mk(0.f, 0.f, 0.f), d = o, att = o;
     uint32_t depth = 0;
     uint64_t rng = 0;
@@ -897,6 +931,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
     // lds_hid[lane] != ~0: the lane's last hit was a dielectric sphere, tested first next segment
     // (hint_candidate); kept in LDS, not in a register (at 72 VGPRs one more value spills)
     lds_hid[thread_slot(wave_base)] = ~0u;
+    // the instrumented kernel: neighbour words that no dielectric hit wrote point past any blob
+    // (hint_candidate's bounds check)
+    if (STATS) lds_nb[thread_slot(wave_base)] = 0x7fff7fffu;
     WaveTally<COUNT> wt;
     Dbg dbg{};
     uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0;
@@ -1026,27 +1063,29 @@ __device__ __forceinline__ void render_body(const KParams &p)
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (!alive && rank < avail) {
-                const uint32_t I = cnext + rank;
+                uint32_t I = cnext + rank;
                 if constexpr (DEEP) {
                     // a queued path resumes where the main launch left it: the ray of its next
                     // segment, attenuation, data stream and segment count; ls = 0 and pix = the
                     // slot index address the same slot
                     const uint32_t cap = 8u * P.deep.rcap;
+                    I = checked<STATS>(I, cap, BC_DEEP_ITEM, p.dbg);
                     const float *f = P.deep.f;
                     o = mk(f[I], f[cap + I], f[2 * cap + I]);
                     d = mk(f[3 * cap + I], f[4 * cap + I], f[5 * cap + I]);
                     att = mk(f[6 * cap + I], f[7 * cap + I], f[8 * cap + I]);
                     rng = P.deep.rng[I];
                     pix = P.deep.slot[I];
-                    ls = 0;
+                    ls = P.deep.link[I];  // the deep launch: ls is the path's pair link
                     depth = P.deep_mode;
                     alive = true;
                     // its hint sphere (hint_candidate): the geo entry from the shading record
                     const uint32_t hid = P.deep.hid[I], sl = thread_slot(wave_base);
+                    lds_park[0][sl] = __uint_as_float(I);
                     if (hid != ~0u) {
                         // (from LDS when the launch staged the shading records there: a lone
                         // deep launch, whose refills then wait on no second global round trip)
-                        const uint32_t ib = hid & 0x7fffffffu;
+                        const uint32_t ib = checked<STATS>(hid & 0x7fffffffu, P.n_spheres, BC_DEEP_HINT, p.dbg);
                         const uint32_t di = P.shade_offset + 2 * P.n_spheres + (P.n_spheres + 15u) / 16u + ib;
                         float4 sf, dr;
                         if (P.shade_lds) {
@@ -1062,8 +1101,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     }
                     lds_hid[sl] = hid;
                 } else {
-                    ls = udiv(I, fc->div_n_pixels);
-                    pix = I - ls * fc->n_pixels;
+                    it = I;  // a pair item (the pass's full blocks) or a single tail sample; its slot
                     alive = fresh = true;
                 }
             }
@@ -1072,15 +1110,88 @@ __device__ __forceinline__ void render_body(const KParams &p)
             need = ballot(!alive);
         }
 
+        // a pair whose first sample ended last iteration: its second sample starts now
+        if (!DEEP && (it & kItRestart)) {
+            fresh = true;
+            it &= ~kItRestart;
+        }
         stamp(0);
         // ---- start the sample of a freshly assigned item (main.cxx:192-200) -----------
         const uint64_t inc_data = ((uint64_t)fc->inc_data_hi << 32) | fc->inc_data_lo;
+        // A sample's colour is final (main.cxx:205 sums it): a single's goes to its slot; a pair's
+        // first is parked in the lane's scratch word and its second sample starts next iteration
+        // (true: the lane sits out the rest of this one); the second's completes the pair sum
+        // RN(c_2j + c_2j+1) in the pair's slot. In the deep launch the path's pair link says where
+        // its partner's colour is.
+        // the pixel (enumeration index) and the sample of the pass of the lane's item word
+        auto item_pixel = [&](uint32_t &s) -> uint32_t {
+            const uint32_t sl = it & kItSlot;
+            const bool pr = sl < P.n_pair_items;
+            const uint32_t J = pr ? sl : sl - P.n_pair_items;
+            const uint32_t q = udiv(J, fc->div_n_pixels);
+            s = pr ? 2u * q + (it >> 31) : 2u * fc->n_pairs + q;
+            return J - q * fc->n_pixels;
+        };
+        auto finish = [&](f3 col) -> bool {
+            float *dst;
+            if constexpr (DEEP) {
+                const uint32_t role = ls >> 30;
+                dst = P.slots + (size_t)checked<STATS>(pix, P.n_items, BC_SLOT, p.dbg) * 3u;
+                if (role == kRolePartnerDone) {
+                    // the partner ended in the main launch and left its colour in the slot
+                    // (IEEE addition is commutative: the order of the pair's two terms is moot)
+                    col = mk(dst[0], dst[1], dst[2]) + col;
+                } else if (role != kRoleSingle) {
+                    // both samples of the pair came here: the second of the two to end sums.
+                    // Each leaves its colour in its own entry (its o.xyz words, read at its
+                    // refill) with device-scope atomics, then counts its arrival at the first's
+                    // entry; the one that finds the other arrived reads that colour back with
+                    // atomics (device-scope atomics are coherent across the XCDs' L2s)
+                    const uint32_t cap = 8u * P.deep.rcap, self = __float_as_uint(lds_park[0][thread_slot(wave_base)]);
+                    const uint32_t partner = ls & kLinkIndex, first = role == kRoleBothFirst ? self : partner;
+                    uint32_t *fw = reinterpret_cast<uint32_t *>(P.deep.f);
+                    const uint32_t r = atomicExch(fw + self, __float_as_uint(col.x)) ^
+                                       atomicExch(fw + cap + self, __float_as_uint(col.y)) ^
+                                       atomicExch(fw + 2u * cap + self, __float_as_uint(col.z));
+                    uint32_t one = 1u;
+                    asm volatile("" : "+v"(one) : "v"(r));  // the arrival after the colour is stored
+                    if (atomicAdd(P.deep.meet + first, one) != 1u) {
+                        alive = false;  // the partner has not ended: it sums
+                        return false;
+                    }
+                    const f3 cp = mk(__uint_as_float(atomicOr(fw + partner, 0u)), __uint_as_float(atomicOr(fw + cap + partner, 0u)),
+                                     __uint_as_float(atomicOr(fw + 2u * cap + partner, 0u)));
+                    col = role == kRoleBothFirst ? col + cp : cp + col;  // RN(c_2j + c_2j+1)
+                    atomicExch(P.deep.meet + first, 0u);               // zero again for the next pass
+                }
+            } else {
+                const uint32_t slot = it & kItSlot;
+                if (slot < P.n_pair_items) {
+                    const uint32_t sl = thread_slot(wave_base);
+                    if (!(it & kItSecond)) {
+                        lds_park[0][sl] = col.x;
+                        lds_park[1][sl] = col.y;
+                        lds_park[2][sl] = col.z;
+                        it |= kItSecond | kItRestart;
+                        return true;
+                    }
+                    // the first's colour, unless it went to the deep queue (which then adds this one)
+                    if (!(it & kItFirstDeep)) col = mk(lds_park[0][sl], lds_park[1][sl], lds_park[2][sl]) + col;  // RN(c_2j + c_2j+1)
+                }
+                dst = P.slots + (size_t)checked<STATS>(slot, P.n_items, BC_SLOT, p.dbg) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
+            }
+            dst[0] = col.x;
+            dst[1] = col.y;
+            dst[2] = col.z;
+            alive = false;
+            return false;
+        };
         uint64_t rc = 0;  // the camera stream of a fresh sample
         float uu = 0.f, vv = 0.f;
         if (fresh) {
             RT_EV(EV_FRESH);
-            uint32_t px, rr;
-            pixel_of(*fc, pix, px, rr);
+            uint32_t px, rr, ls;
+            pixel_of(*fc, item_pixel(ls), px, rr);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
             const uint32_t s = fc->sample_begin + ls;
             // key = (y W + x) spp + s (y W + x < 2^32: the host bounds W H)
@@ -1120,6 +1231,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
         // waits for its unluckiest lane's whole run (mean 1.91 attempts, ~6.9 for the worst of
         // 64 lanes), and every stream still sees the same draws in the same order.
         bool defer = false;
+        bool absorbed = false;  // a metal scatter absorbed: colour 0, finished at the iteration's end
         const bool lens = !DEEP && (fresh || pend_lens);
         if (lens || pend) {
             const uint64_t inc = lens ? (((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo) : inc_data;
@@ -1165,15 +1277,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                         d = nd;
                     } else {                               // absorbed: main.cxx:68, colour 0
                         RT_EV(EV_METAL_ABSORB);
-                        alive = false;
-                        float *dst = P.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
-                        // zeros made here (left to itself the allocator parks a zero triple in
-                        // scratch for this rare path)
-                        float z = 0.f;
-                        asm volatile("" : "+v"(z));
-                        dst[0] = z;
-                        dst[1] = z;
-                        dst[2] = z;
+                        absorbed = defer = true;  // it traces nothing more
                     }
                 }
                 pend = false;
@@ -1209,16 +1313,45 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 }
                 if (dv && j < P.deep.rcap) {
                     const uint32_t cap = 8u * P.deep.rcap;
-                    j += r * P.deep.rcap;
+                    j = checked<STATS>(j + r * P.deep.rcap, cap, BC_DEEP_APPEND, p.dbg);
+                    uint32_t ss;
+                    const uint32_t px = checked<STATS>(item_pixel(ss), fc->n_pixels, BC_DEEP_PX, p.dbg);
                     float *f = P.deep.f;
                     f[j] = o.x; f[cap + j] = o.y; f[2 * cap + j] = o.z;
                     f[3 * cap + j] = d.x; f[4 * cap + j] = d.y; f[5 * cap + j] = d.z;
                     f[6 * cap + j] = att.x; f[7 * cap + j] = att.y; f[8 * cap + j] = att.z;
                     P.deep.rng[j] = rng;
-                    P.deep.slot[j] = ls * fc->n_pixels + pix;
                     P.deep.hid[j] = lds_hid[thread_slot(wave_base)];
-                    P.deep.px[pix] = 1;
-                    alive = false;
+                    P.deep.px[px] = 1;
+                    // the path's slot and pair link (rt_device.h kRole*)
+                    const uint32_t slot = it & kItSlot, sl = thread_slot(wave_base);
+                    uint32_t link = kRoleSingle << 30;
+                    if (slot >= P.n_pair_items) {
+                        alive = false;
+                    } else {
+                        link = kRolePartnerDone << 30;
+                        if (!(it & kItSecond)) {
+                            // the pair's first: the lane traces the second next iteration, which
+                            // leaves its colour in the slot (or joins this one in the queue)
+                            lds_park[0][sl] = __uint_as_float(j);
+                            it |= kItSecond | kItFirstDeep | kItRestart;
+                            defer = true;  // sits out the rest of this iteration
+                        } else {
+                            if (it & kItFirstDeep) {  // both of the pair queued: they meet there
+                                const uint32_t j1 = __float_as_uint(lds_park[0][sl]);
+                                link = (kRoleBothSecond << 30) | j1;
+                                P.deep.link[j1] = (kRoleBothFirst << 30) | j;
+                            } else {  // the first's colour, parked in the lane's LDS words, to the slot
+                                float *dst = P.slots + (size_t)checked<STATS>(slot, P.n_items, BC_SLOT, p.dbg) * 3u;
+                                dst[0] = lds_park[0][sl];
+                                dst[1] = lds_park[1][sl];
+                                dst[2] = lds_park[2][sl];
+                            }
+                            alive = false;
+                        }
+                    }
+                    P.deep.slot[j] = slot;
+                    P.deep.link[j] = link;
                 }
             }
         }
@@ -1255,7 +1388,8 @@ __device__ __forceinline__ void render_body(const KParams &p)
             const uint32_t sl = thread_slot(wave_base);
             const uint32_t hid = lds_hid[sl];
             if (ballot(seg && hid != ~0u))
-                key0 = hint_candidate<FAST>(seg && hid != ~0u, lds_pn[sl], hid, lds_nb[sl], geo, sidx, o, d, rd, P.iso, skip);
+                key0 = hint_candidate<FAST, STATS>(seg && hid != ~0u, lds_pn[sl], hid, lds_nb[sl], geo, sidx, o, d, rd, P.iso,
+                                                   skip, P.n_geo, P.diag_unbounded_nb, p.dbg);
             const bool walk = seg && !skip;
             const uint64_t wm = ballot(walk);
             if (STATS && first_active_lane()) {
@@ -1275,14 +1409,14 @@ __device__ __forceinline__ void render_body(const KParams &p)
         }
 
         // ---- shading: the hit of every live lane -----------------------------------------
+        bool done = absorbed;
+        f3 col = mk(0.f, 0.f, 0.f);
         if (alive && !defer) {
-            bool done = false;
-            f3 col = mk(0.f, 0.f, 0.f);
             if (!seg) {
                 done = true;  // main.cxx:74 (only reachable with max_depth == 0)
             } else {
                 const float t = h.t();
-                const uint32_t ib = h.id();
+                uint32_t ib = h.id();
                 ++depth;
                 if (ib == 0xffffffffu) {
                     RT_EV(EV_SKY);
@@ -1308,6 +1442,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     done = true;
                 } else {
                     RT_EV(EV_HIT);
+                    ib = checked<STATS>(ib, P.n_spheres, BC_SHADE, p.dbg);
                     float4 sf, md;
                     uint32_t kind;
                     if (V != V_EXACT_SCALAR && P.shade_lds) {
@@ -1389,16 +1524,12 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 }
             }
             stamp(3);
-            if (done) {
-                RT_EV(EV_STORE);
-                // the sample's colour goes to its slot; accumulate_kernel forms the reference's
-                // blocked sum over the slots (main.cxx:205)
-                alive = false;
-                float *dst = P.slots + (size_t)(ls * fc->n_pixels + pix) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
-                dst[0] = col.x;
-                dst[1] = col.y;
-                dst[2] = col.z;
-            }
+        }
+        if (done) {
+            RT_EV(EV_STORE);
+            // the sample's colour goes to its slot or its pair; accumulate_kernel forms the
+            // reference's blocked sum over the slots (main.cxx:205)
+            finish(col);
         }
     }
 
@@ -1431,15 +1562,17 @@ __device__ __forceinline__ void render_body(const KParams &p)
             atomicMax(p.dbg + 14, ~t_wave0);  // launch start = ~max(~t) = earliest wave start
         }
         // wave timeline: [16 + 4w] time the queues were found dry (realtime ticks), [17 + 4w] exit,
-        // [18 + 4w] loop iterations, [19 + 4w] hardware id << 32 | iterations after dry << 16 |
-        // refill rounds; w = wave of the grid. The launch starts at t_wave0 of the earliest wave.
+        // [18 + 4w] shader-clock cycles in the loop << 32 | refill rounds << 16 | loop iterations,
+        // [19 + 4w] hardware id << 48 | iterations after dry << 32 | the wave's start (low 32 bits of
+        // the realtime clock); w = wave of the grid. The launch starts at t_wave0 of the earliest wave.
         const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (lane == 0 && w < kDbgWaves) {
+            const unsigned long long cy = cyc[0] + cyc[1] + cyc[2] + cyc[3] + cyc[4];
             p.dbg[16 + 4 * w] = t_dry ? t_dry : __builtin_amdgcn_s_memrealtime();
             p.dbg[17 + 4 * w] = __builtin_amdgcn_s_memrealtime();
-            p.dbg[18 + 4 * w] = dbg_iters;
-            p.dbg[19 + 4 * w] = ((unsigned long long)__smid() << 32) | (min(dbg_iters_dry, 65535u) << 16) |
-                                min(dbg_refills, 65535u);
+            p.dbg[18 + 4 * w] = (min(cy, 0xffffffffull) << 32) | (min(dbg_refills, 65535u) << 16) | min(dbg_iters, 65535u);
+            p.dbg[19 + 4 * w] = ((unsigned long long)(__smid() & 0xffffu) << 48) |
+                                ((unsigned long long)min(dbg_iters_dry, 65535u) << 32) | (uint32_t)t_wave0;
         }
     }
 }
@@ -1671,9 +1804,15 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
         const float *v = k.slots + ((size_t)s * k.n_pixels + i) * 3u;
         return mk(v[0], v[1], v[2]);
     };
-    uint32_t s = 0;
-    for (; s < 4u * k.n_blocks; s += 4u) acc = acc + ((ld(s) + ld(s + 1u)) + (ld(s + 2u) + ld(s + 3u)));
-    for (; s < k.n_samples; ++s) acc = acc + ld(s);
+    if (k.paired) {
+        // pair sums: slot 2b holds c0+c1, slot 2b+1 c2+c3 of block b; then the tail's samples
+        for (uint32_t b = 0; b < k.n_blocks; ++b) acc = acc + (ld(2u * b) + ld(2u * b + 1u));
+        for (uint32_t t = 4u * k.n_blocks; t < k.n_samples; ++t) acc = acc + ld(t - 2u * k.n_blocks);
+    } else {
+        uint32_t s = 0;
+        for (; s < 4u * k.n_blocks; s += 4u) acc = acc + ((ld(s) + ld(s + 1u)) + (ld(s + 2u) + ld(s + 3u)));
+        for (; s < k.n_samples; ++s) acc = acc + ld(s);
+    }
     if (!k.last) {
         k.acc[3 * i] = acc.x; k.acc[3 * i + 1] = acc.y; k.acc[3 * i + 2] = acc.z;
         return;

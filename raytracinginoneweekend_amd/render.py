@@ -221,7 +221,7 @@ class DeviceScene:
         """rt_scene_usage_get: device bytes held and the last render's cut, as a dict."""
         u = abi.RtSceneUsage()
         check(lib().rt_scene_usage_get(self.handle, C.byref(u)))
-        return {k: getattr(u, k) for k, _ in abi.RtSceneUsage._fields_ if k != "reserved"}
+        return {k: getattr(u, k) for k, _ in abi.RtSceneUsage._fields_}
 
     def kernel_times(self, max_calls=256):
         """Render-kernel durations (ms) of the most recent render() calls, oldest first."""
@@ -252,14 +252,21 @@ class DeviceScene:
         return dict(zip(self.EVENTS, list(buf)))
 
     def debug_timeline(self, max_waves=65536):
-        """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry) of the last
-        instrumented launch (options stats=True; dry = when the wave found every queue empty; times
-        in ticks of the 100 MHz clock), see rt_scene_debug_timeline."""
+        """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry, start, cycles) of the
+        last instrumented launch (options stats=True; dry = when the wave found every queue empty;
+        times in ticks of the 100 MHz clock; cycles = shader-clock cycles in the loop, so
+        cycles / (exit - start) x 100 MHz is the clock the wave ran at), see rt_scene_debug_timeline."""
         buf = (C.c_uint64 * (4 * max_waves))()
         n = C.c_uint32(0)
         check(lib().rt_scene_debug_timeline(self.handle, buf, max_waves, C.byref(n)))
-        return [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], buf[4 * i + 3] >> 32, buf[4 * i + 3] & 0xffff,
-                 (buf[4 * i + 3] >> 16) & 0xffff) for i in range(n.value)]
+        out = []
+        for i in range(n.value):
+            dry, ex, a, b = buf[4 * i], buf[4 * i + 1], buf[4 * i + 2], buf[4 * i + 3]
+            start = (ex & ~0xffffffff) | (b & 0xffffffff)  # the start's low 32 bits, in the exit's epoch
+            if start > ex:
+                start -= 1 << 32
+            out.append((dry, ex, a & 0xffff, b >> 48, (a >> 16) & 0xffff, (b >> 32) & 0xffff, start, a >> 32))
+        return out
 
     def close(self):
         if self.handle:

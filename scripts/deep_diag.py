@@ -30,6 +30,10 @@ cam = rt.Camera.default(W, H)
 p = rt.make_params(W, H, spp, depth, 1234)
 out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 stream = torch.cuda.current_stream().cuda_stream
+def _qs(v):
+    return [round(v[min(len(v) - 1, int(f * len(v)))], 3) if v else None for f in (0.0, 0.1, 0.5, 0.9, 1.0)]
+
+
 for text in a.options:
     o = rt.parse_options(text, rt.options(rt.default_options(), stats=True, stats_deep_only=True))
     ds = rt.DeviceScene(arrays, options=o)
@@ -50,6 +54,13 @@ for text in a.options:
            "wave_iters": c["wave_iters"], "refills": c["wave_refills"],
            "cycle_share": {k: round(c[k] / max(1, cyc), 3) for k in ("cyc_refill", "cyc_start", "cyc_hit", "cyc_shade", "cyc_fold")},
            "cycles_per_wave_iter": round(cyc / max(1, c["wave_iters"]), 1),
+           # shader clock seen by the waves: their s_memtime cycles over their s_memrealtime life
+           # (every wave of the resident grid starts at the launch's start)
+           "clock_ghz_busy_waves": {f"p{int(f * 100)}": v for f, v in zip(
+               (0.0, 0.1, 0.5, 0.9, 1.0), _qs(sorted(r[7] / max(1, r[1] - r[6]) * 0.1 for r in busy)))},
+           "us_per_busy_iter": {f"p{int(f * 100)}": v for f, v in zip(
+               (0.0, 0.1, 0.5, 0.9, 1.0), _qs(sorted((r[1] - r[6]) / 100.0 / max(1, r[2]) for r in busy)))},
+           "busy_wave_start_us": {f"p{int(f * 100)}": q(sorted(r[6] - t0 for r in busy), f) for f in (0.0, 0.5, 1.0)},
            "events": {k: int(v) for k, v in ev.items() if v},
            "busy_wave_exit_us": {f"p{int(f * 100)}": q(ends, f) for f in (0.0, 0.1, 0.5, 0.9, 0.99, 1.0)},
            "busy_wave_dry_us": {f"p{int(f * 100)}": q(sorted(r[0] - t0 for r in busy), f) for f in (0.0, 0.1, 0.5, 0.9, 1.0)},

@@ -19,6 +19,11 @@ step() {  # step <name> <seconds> <cmd...>
 for s in ${STEPS:-smoke pytest bench prof}; do
   case $s in
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    probe)  step probe 60 ./scripts/_bin/lds_oob_probe ;;
+    new)    step new 600 python -u -m pytest ${NEW_TESTS:-tests} -m gpu -v --timeout 200 --timeout-method thread ;;
+    rehearse) for n in ${REHEARSE_N:-2 4 8}; do
+                step rehearse_n$n 600 python bench.py --rehearse-world $n --rehearse-gather --no-cpu-baseline --corrected-steps 0 ${BENCH_ARGS:-}
+              done ;;
     pytest) step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stock)  step stock 600 python bench.py --hw-queues 0 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;

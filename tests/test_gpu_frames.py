@@ -91,6 +91,40 @@ def test_baseline_frame_stream_matches_reference(cfg):
     assert int(seg[0]) > W * H * spp  # every primary plus its bounces
 
 
+def test_bounds_checked_frame_stream_c3():
+    """Round 4's hipErrorIllegalAddress, pinned. The instrumented kernel
+    (options stats=True) checks every lane-computed index into the scene blob, the sample slots
+    and the deep queue before it uses it, and starts every lane's walk-shortcut neighbour word
+    at 0x7fff7fff (slots past any blob), as a stale or never-written word may hold. Over the
+    config-3 frame stream (a lone first frame with its 8-wave deep launch, then frames in flight
+    with 4-wave deep launches and global shading records) no index passes its bound, and the
+    frames equal the reference's. With unbounded_nb the neighbour slots are formed without the
+    lane's own bound, as before fd383c3: the check then reports them (and reads slot 0 instead,
+    so the frames are unchanged) — the bound is what keeps those reads inside the blob."""
+    torch = pytest.importorskip("torch")
+    ref = _full_ref("c3")
+    W, H, spp, depth = ref["width"], ref["height"], ref["spp"], ref["depth"]
+    s, m = G.scene(ref["scene"])
+    p = rt.make_params(W, H, spp, depth, ref["seed"])
+    cam = rt.Camera.default(W, H)
+    stream = torch.cuda.current_stream().cuda_stream
+    for unbounded in (False, True):
+        ds = rt.DeviceScene((s, m), options=rt.options(rt.default_options(), stats=True, unbounded_nb=unbounded))
+        outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(3)]
+        for o in outs:
+            ds.render(cam, p, o.data_ptr(), stream)
+        torch.cuda.synchronize()
+        if unbounded:
+            with pytest.raises(rt.RtError, match="neighbour slot"):
+                ds.debug_counters()
+        else:
+            c = ds.debug_counters()
+            assert c["wave_iters"] > 0
+        ds.close()
+        for k, o in enumerate(outs):
+            _assert_frame_digest(o.cpu().numpy(), ref, f"c3 instrumented frame {k} (unbounded_nb={unbounded})")
+
+
 @pytest.mark.parametrize("cfg", sorted(FULL))
 def test_full_config_frame_matches_reference_rows(cfg):
     c = FULL[cfg]
@@ -344,6 +378,97 @@ def test_deep_split_overflow_feedback(opts):
 
 
 
+@pytest.mark.parametrize("streams", [1, 0])
+def test_sample_pairs_through_the_deep_queue(streams, opts):
+    """Sample pairs whose samples leave for the deep queue: with the split at 1
+    segment most continuing paths go there, so pairs end with one sample in each launch (the
+    first's or the second's colour left in the pair slot) or with both queued (they meet through
+    device-scope atomics, the second to end sums). Frames of different sizes and sample counts
+    (pairs and single tail samples, several passes) follow each other on one scene, so every
+    workspace's deep queue is laid out anew between passes (its pair-arrival words must start at
+    zero); one workspace (render_streams = 1) or the default rotation. Each frame equals the
+    oracle bit for bit, as does the unpaired render (no_pairs)."""
+    torch = pytest.importorskip("torch")
+    s, m = _glass_scene_frames()
+    # one pass budget for the scene (8 samples of the largest frame): the frames below are cut
+    # into passes of different sizes, single tail samples included
+    opts.set(deep_min_items=0, deep_split=1, render_streams=streams, max_pass_bytes=80 * 44 * 12 * 8)
+    cases = [(64, 40, 10), (48, 30, 23), (80, 44, 16), (40, 24, 7), (64, 40, 10), (80, 44, 26)]
+    ds = rt.DeviceScene((s, m))
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for W, H, spp in cases:
+        o = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        ds.render(rt.Camera.default(W, H), rt.make_params(W, H, spp, 64, 31), o.data_ptr(), stream)
+        outs.append(o)
+    torch.cuda.synchronize()
+    ds.close()
+    for (W, H, spp), o in zip(cases, outs):
+        want, _ = O.render_f32(s, m, O.camera_default(W, H), rt.make_params(W, H, spp, 64, 31))
+        _bits_equal(o.cpu().numpy(), want, f"{W}x{H} spp {spp}")
+    opts.set(no_pairs=True)
+    W, H, spp = cases[1]
+    img, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 31))
+    want, _ = O.render_f32(s, m, O.camera_default(W, H), rt.make_params(W, H, spp, 64, 31))
+    _bits_equal(img, want, "no_pairs")
+
+
+def _glass_scene_frames():
+    """Small glass balls on the ground in front of the reference camera (rays trapped in them
+    run to max_depth), a big glass sphere, lambert and metal balls."""
+    rng = np.random.default_rng(5)
+    n = 160
+    s = np.zeros(n, dtype=abi.SPHERE_DTYPE)
+    m = np.zeros(4, dtype=abi.MATERIAL_DTYPE)
+    m[0] = (0, [0.5, 0.5, 0.5], 0.0)
+    m[1] = (1, [0.7, 0.6, 0.5], 0.05)
+    m[2] = (2, [1.0, 1.0, 1.0], 1.5)
+    m[3] = (0, [0.8, 0.3, 0.2], 0.0)
+    r = rng.choice([0.2, 0.3, 0.15], n).astype(np.float32)
+    c = np.zeros((n, 3), dtype=np.float32)
+    c[:, 0] = rng.uniform(-6, 6, n)
+    c[:, 2] = rng.uniform(-6, 6, n)
+    c[:, 1] = r
+    s["center"], s["radius"], s["material"] = c, r, rng.choice([2, 2, 2, 0, 1, 3], n)
+    s["center"][0], s["radius"][0], s["material"][0] = (0, -1000, 0), 1000.0, 0
+    s["center"][1], s["radius"][1], s["material"][1] = (0, 1, 0), 1.0, 2
+    return s, m
+
+
+def test_lone_deep_launch_static_dealing_runs(opts):
+    """The lone pass's deep launch (8-wave workgroups, shading records in LDS, chunks dealt
+    statically from the regions' final counts) is taken when a split pass runs alone with the
+    main launch's shading records in global memory, and reported by rt_scene_usage.deep_launch
+    (8 | 16); frames in flight take the 4-wave launch (4). Both equal the unsplit render bit for
+    bit, with the same segment counts (no test checked that the static path ran)."""
+    torch = pytest.importorskip("torch")
+    opts.set(deep_min_items=0, shade_global=True)
+    s, m = G.scene("huge")
+    W, H, spp = 640, 360, 64  # ~0.8 ms a frame: the next call arrives while it runs
+    cam = rt.Camera.default(W, H)
+    p = rt.make_params(W, H, spp, 64, 17)
+    opts.set(deep_split=0)
+    want, want_st = rt.render_f32((s, m), p, cam)
+    opts.set(deep_split=8)
+    ds = rt.DeviceScene((s, m))
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(4)]
+    segs = [torch.zeros(3, dtype=torch.int64, device="cuda") for _ in range(4)]
+    ds.render(cam, p, outs[0].data_ptr(), stream, segs[0].data_ptr())
+    torch.cuda.synchronize()
+    lone = ds.usage()["deep_launch"]
+    for o, g in zip(outs[1:], segs[1:]):  # back to back: the later ones start while others run
+        ds.render(cam, p, o.data_ptr(), stream, g.data_ptr())
+    flight = ds.usage()["deep_launch"]
+    torch.cuda.synchronize()
+    ds.close()
+    assert lone == 8 | 16, lone
+    assert flight == 4, flight
+    for k, (o, g) in enumerate(zip(outs, segs)):
+        _bits_equal(o.cpu().numpy(), want, f"frame {k}")
+        assert int(g[0]) == want_st.segments
+
+
 @pytest.mark.parametrize("streams", [0, 1])
 def test_deep_split_variants_and_row_shares(streams, opts):
     """The split with the render variants (fast-math; brute force, the scalar-cache scene and the
@@ -461,7 +586,9 @@ def test_workspace_cap_bounds_memory_with_the_same_bits(opts):
             assert int(g[0]) == want_st.segments
         if cap:
             assert u["workspace_bytes"] <= cap, (cap, u)
-        assert u["workspace_bytes"] >= u["workspaces"] * u["pass_samples"] * per_sample
+        # a pass's slots: two sample pairs per full block of 4, one slot per tail sample
+        ps = u["pass_samples"]
+        assert u["workspace_bytes"] >= u["workspaces"] * (ps - 2 * (ps // 4)) * per_sample
         seen.add((u["render_streams"], u["workspaces"], u["pass_samples"]))
     assert len(seen) >= 3  # the caps changed the cut
     ds = rt.DeviceScene((s, m), options=rt.options(max_workspace_bytes=100 << 10))

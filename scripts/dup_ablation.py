@@ -34,12 +34,12 @@ PATCHES = {
                "                const bool bs2 = box_pass(rb, s0b, s1, t_lo, h.t() * 1.002f);\n"
                "                asm volatile(\"\" ::\"v\"((uint32_t)bs2));\n"
                "            }\n"),
-    "ground": ("    run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o, d, rd, h, dbg);\n",
+    "ground": ("    if (RT_GROUND1 && p.n_always == 1u) test_block8<FAST, STATS, 1>(geo, sidx, 0, o, d, rd, h, dbg);\n",
                "    {\n"
                "        f3 o2 = o;\n"
                "        asm volatile(\"\" : \"+v\"(o2.x));\n"
                "        Hit h2{key0};\n"
-               "        run_members<FAST, STATS>(geo, sidx, 0, p.n_always, o2, d, rd, h2, dbg);\n"
+               "        test_block8<FAST, STATS, 1>(geo, sidx, 0, o2, d, rd, h2, dbg);\n"
                "        asm volatile(\"\" ::\"v\"((uint32_t)h2.key), \"v\"((uint32_t)(h2.key >> 32)));\n"
                "    }\n"),
 }
@@ -68,6 +68,38 @@ PATCHES.update({
                 "                                const float p2 = schlick_x(xs, cosv + u2.x * 0.f);\n"
                 "                                asm volatile(\"\" ::\"v\"(r2.x), \"v\"(r2.y), \"v\"(r2.z), \"v\"(p2));\n"
                 "                            }\n"),
+    # the fresh sample start: item -> pixel, sample, key, seeds, two jitter draws, uu vv
+    "start": ("            att = mk(1.f, 1.f, 1.f);\n            depth = 0;\n",
+              "            {\n"
+              "                uint32_t it2 = it;\n"
+              "                asm volatile(\"\" : \"+v\"(it2));\n"
+              "                const uint32_t sl2 = it2 & kItSlot;\n"
+              "                const bool pr2 = sl2 < P.n_pair_items;\n"
+              "                const uint32_t J2 = pr2 ? sl2 : sl2 - P.n_pair_items;\n"
+              "                const uint32_t q2 = udiv(J2, fc->div_n_pixels);\n"
+              "                const uint32_t ls2 = pr2 ? 2u * q2 + (it2 >> 31) : 2u * fc->n_pairs + q2;\n"
+              "                uint32_t px2, rr2;\n"
+              "                pixel_of(*fc, J2 - q2 * fc->n_pixels, px2, rr2);\n"
+              "                const uint32_t py2 = fc->row_offset + rr2 * fc->row_stride;\n"
+              "                const uint64_t key2 = (uint64_t)(py2 * fc->W + px2) * fc->spp + fc->sample_begin + ls2;\n"
+              "                uint64_t rng2 = key2 * kPcgMul + inc_data * (kPcgMul + 1u);\n"
+              "                const float xu2 = canonical(rng2, inc_data);\n"
+              "                const float xv2 = canonical(rng2, inc_data);\n"
+              "                const float uu2 = div_const((float)px2, fc->fW, fc->rW, true) + div_const(xu2, fc->fW, fc->rW, true);\n"
+              "                const float vv2 = div_const((float)py2, fc->fH, fc->rH, true) + div_const(xv2, fc->fH, fc->rH, true);\n"
+              "                asm volatile(\"\" ::\"v\"(uu2), \"v\"(vv2), \"v\"((uint32_t)rng2));\n"
+              "            }\n"),
+    # hit shading for metal/dielectric lanes: hit point, normal, unit direction, reflection
+    "shade": ("                        const f3 rf = reflect(ud, hn);\n",
+              "                        {\n"
+              "                            f3 d2 = d;\n"
+              "                            asm volatile(\"\" : \"+v\"(d2.x));\n"
+              "                            const f3 dv2 = (o + d2 * t) - ctr;\n"
+              "                            const f3 hn2 = (P.fast_roots && all_lanes_min_abs_ok(dv2)) ? div3_short(dv2, sf.w) : dv2 / sf.w;\n"
+              "                            const f3 ud2 = (rd.fd != 0u && all_lanes_min_abs_ok(d2)) ? div3_short(d2, sqrt_scaled(a)) : normalize(d2);\n"
+              "                            const f3 rf2 = reflect(ud2, hn2);\n"
+              "                            asm volatile(\"\" ::\"v\"(rf2.x), \"v\"(rf2.y), \"v\"(rf2.z));\n"
+              "                        }\n"),
 })
 ONLY = os.environ.get("DUP_ONLY", "").split(",") if os.environ.get("DUP_ONLY") else None
 FLAGS = ["-std=c++17", "-O3", "-fno-slp-vectorize", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math",
@@ -79,7 +111,7 @@ for name, (anchor, extra) in PATCHES.items():
     src = os.path.join(out, "src")
     shutil.rmtree(out, ignore_errors=True)
     os.makedirs(src)
-    for f in ("rt_kernel.hip", "rt_host.cpp", "rt_device.h"):
+    for f in ("rt_kernel.hip", "rt_device.h", "rt_consts.h"):
         shutil.copy(os.path.join(SRC, f), src)
     os.makedirs(os.path.join(out, "include"), exist_ok=True)
     text = open(os.path.join(src, K)).read()
@@ -97,6 +129,6 @@ for name, (anchor, extra) in PATCHES.items():
     # the host side is unchanged: the product build's object (make -C raytracinginoneweekend_amd/csrc)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                     os.path.join(out, "librt_mi355x.so"), os.path.join(out, "k.o"), os.path.join(SRC, "_obj", "rt_host.o"),
-                    "-Wl,--no-undefined"], check=True)
+                    os.path.join(SRC, "_obj", "rt_host_build.o"), "-Wl,--no-undefined"], check=True)
     shutil.rmtree(src)
     print("built", out)

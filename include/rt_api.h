@@ -301,7 +301,8 @@ int rt_scene_kernel_times(rt_scene *scene, uint32_t max, float *ms, uint32_t *n)
  * [1] wave refill rounds, [2] wave / [3] lane sphere blocks with a positive discriminant,
  * [4] wave / [5] lane root evaluations, [6] segments, [7] wave-level blocks of 8 cluster
  * members executed, [8..12] shader-clock cycles summed over waves per loop region
- * (refill, sample start + rejection loop, closest hit, shading, fold), [14] ~(earliest wave
+ * (refill, sample start + rejection loop, closest hit, shading, fold), [13] items dealt (the
+ * deep launch: queued paths), [14] ~(earliest wave
  * start, 100 MHz clock), [15] the bounds check's first violation, code << 32 | index
  * (rt_device.h BoundsCode; 0 = none). Copies them out; reset zeroes. Returns RT_ERR_DEVICE
  * (the message names the index) when [15] is set: the instrumented kernel checks every

@@ -285,9 +285,6 @@ struct scene_builder {
         sph(-2.f, 1.f, 0.f, 1.f, 2);
         sph(-2.f, 1.f, 0.f, -.99f, 2);
     }
-    // src/main.cxx:131-177 (namespace typo fixed). Draw order: type, center.x, center.z, then
-    // the material's draws; a type-3 sphere pushes no material, so it shares the index of the
-    // next pushed one and trailing ones are resolved by default materials (lambert, albedo 1).
     void cuda_variant()  // src/CUDA/cuda_impl.cu:425-437
     {
         mat(RT_LAMBERT, static_cast<float>(.1), static_cast<float>(.2), static_cast<float>(.5), 0.f);
@@ -300,6 +297,9 @@ struct scene_builder {
         sph(-1.f, 0.f, -1.f, .5f, 2);
         sph(-1.f, 0.f, -1.f, -.499f, 2);
     }
+    // src/main.cxx:131-177 (namespace typo fixed). Draw order: type, center.x, center.z, then
+    // the material's draws; a type-3 sphere pushes no material, so it shares the index of the
+    // next pushed one and trailing ones are resolved by default materials (lambert, albedo 1).
     void huge(uint32_t seed)
     {
         simple();

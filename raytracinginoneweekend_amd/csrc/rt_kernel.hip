@@ -936,7 +936,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
     if (STATS) lds_nb[thread_slot(wave_base)] = 0x7fff7fffu;
     WaveTally<COUNT> wt;
     Dbg dbg{};
-    uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0;
+    uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0, dbg_dealt = 0;
     uint64_t t_dry = 0;  // STATS: realtime when this wave found every queue empty
     // STATS build only: shader-clock cycles per loop region, summed over the wave's iterations
     uint64_t cyc[5] = {0, 0, 0, 0, 0};  // refill, sample start, closest hit, shading, fold
@@ -1106,6 +1106,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 }
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
+            if (STATS) dbg_dealt += took;
             cnext += took;
             need = ballot(!alive);
         }
@@ -1560,6 +1561,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
         if (lane == 0) {
             for (int i = 0; i < 5; ++i) atomicAdd(p.dbg + 8 + i, (unsigned long long)cyc[i]);
             atomicMax(p.dbg + 14, ~t_wave0);  // launch start = ~max(~t) = earliest wave start
+            atomicAdd(p.dbg + 13, (unsigned long long)dbg_dealt);  // items (deep: paths) dealt
         }
         // wave timeline: [16 + 4w] time the queues were found dry (realtime ticks), [17 + 4w] exit,
         // [18 + 4w] shader-clock cycles in the loop << 32 | refill rounds << 16 | loop iterations,

@@ -237,6 +237,7 @@ class DeviceScene:
         keys = ["wave_iters", "wave_refills", "wave_blocks", "lane_blocks", "wave_roots", "lane_roots", "segments",
                 "wave_member_blocks", "cyc_refill", "cyc_start", "cyc_hit", "cyc_shade", "cyc_fold"]
         out = dict(zip(keys, list(buf)))
+        out["items_dealt"] = buf[13]  # items (the deep launch: queued paths) the waves took
         out["launch_start"] = (~buf[14]) & 0xffffffffffffffff if buf[14] else 0  # 100 MHz ticks
         return out
 

@@ -68,5 +68,14 @@ for text in a.options:
                                  for f in (0.0, 0.1, 0.5, 0.9, 1.0)},
            "iters_per_busy_wave": {f"p{int(f * 100)}": (sorted(r[2] for r in busy)[min(len(busy) - 1, int(f * len(busy)))] if busy else None)
                                    for f in (0.0, 0.5, 0.9, 1.0)}}
+    res["paths_dealt"] = c.get("items_dealt", 0)
+    res["segments"] = c["segments"]
+    its = sorted(r[2] for r in busy)
+    hist = {}
+    for v in its:
+        hist[v // 8 * 8] = hist.get(v // 8 * 8, 0) + 1
+    res["iters_hist_by8"] = dict(sorted(hist.items()))
+    res["refills_per_busy_wave"] = {f"p{int(f * 100)}": (sorted(r[4] for r in busy)[min(len(busy) - 1, int(f * len(busy)))] if busy else None)
+                                    for f in (0.0, 0.5, 0.9, 1.0)}
     print(json.dumps(res), flush=True)
     ds.close()

@@ -191,13 +191,13 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-# the timed kernels: rt::render_kernel<0, 7, false, false> (main launch) and
+# the timed kernels: rt::render_kernel<0, 7, false, false, false> (main launch, single samples) and
 # rt::render_deep_kernel<0, false, false, 4 | 8> (the deep launch of a split pass: 4-wave groups
 # beside other renders, 8-wave groups for a lone pass)
-TIMED_KERNEL = ("_ZN2rt13render_kernelILi0ELi7ELb0ELb0EEEvNS_7KParamsE",
+TIMED_KERNEL = ("_ZN2rt13render_kernelILi0ELi7ELb0ELb0ELb0EEEvNS_7KParamsE",
                 "_ZN2rt18render_deep_kernelILi0ELb0ELb0ELi4EEEvNS_7KParamsE",
                 "_ZN2rt18render_deep_kernelILi0ELb0ELb0ELi8EEEvNS_7KParamsE")
-TIMED_KERNEL_NAMES = "render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false, 4|8>"
+TIMED_KERNEL_NAMES = "render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8>"
 
 
 def hashlib_sha256(b):
@@ -615,7 +615,7 @@ def main():
         }
         v = {"exact": 0, "scalar": 1, "fast": 2, "wavefront": 0}[args.variant]
         cull = 0 if args.traversal == "brute" or v == 1 else 7
-        kname = TIMED_KERNEL_NAMES if (v, cull) == (0, 7) else f"render_kernel<{v}, {cull}, false, false>"
+        kname = TIMED_KERNEL_NAMES if (v, cull) == (0, 7) else f"render_kernel<{v}, {cull}, false, false, false>"
         pmc, status = pmc_fields(args.pmc, kname, {"workload": WORKLOAD[args.config], "camera": args.camera,
                                                    "traversal": args.traversal, "n_gpus": world})
         if args.variant == "wavefront":  # other kernels did the work: no render_kernel PMC

@@ -177,7 +177,9 @@ enum rt_diag {
     RT_DIAG_UNBOUNDED_NB = 1u << 10,    /* with STATS: the walk shortcut's neighbour slots formed
                                           without the lane's own bound (the pre-fd383c3 form),
                                           for the bounds check to report (rt_scene_debug_counters) */
-    RT_DIAG_NO_PAIRS = 1u << 11         /* one sample per item and slot (no sample pairs)       */
+    RT_DIAG_NO_PAIRS = 1u << 11,        /* one sample per item and slot, under a cap too        */
+    RT_DIAG_PAIRS = 1u << 12            /* sample pairs for passes in flight without a cap
+                                          (otherwise taken only under max_workspace_bytes)    */
 };
 int rt_options_default(rt_options *out);
 /* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,

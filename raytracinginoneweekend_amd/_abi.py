@@ -78,7 +78,7 @@ class RtSceneUsage(C.Structure):
 RT_DIAG = {
     "ieee_roots": 1 << 0, "no_shortcut": 1 << 1, "no_neighbours": 1 << 2, "no_root_box": 1 << 3,
     "shade_lds": 1 << 4, "shade_global": 1 << 5, "stats": 1 << 6, "stats_deep_only": 1 << 7, "verbose": 1 << 8,
-    "standin_transport": 1 << 9, "unbounded_nb": 1 << 10, "no_pairs": 1 << 11,
+    "standin_transport": 1 << 9, "unbounded_nb": 1 << 10, "no_pairs": 1 << 11, "pairs": 1 << 12,
 }
 
 

@@ -742,11 +742,15 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // (14 workspaces, 24-sample passes), 2.56 uncapped (19.1 GiB; profiles/r04).
     const uint64_t per_sample = n_pixels * 12ull;
     // Sample pairs: a pass's full blocks of 4 samples take two pair slots each,
-    // its tail samples one. Passes issued while other renders run take pairs (half the slot
-    // memory and traffic, the same frame period); a pass issued alone (a lone frame) takes single
+    // its tail samples one: half the slot memory. Their bookkeeping costs the main launch ~3% of
+    // the frame period (profiles/r05/ab/pairs_cost.txt), so they are taken under a workspace cap
+    // (after one workspace per stream, before shorter passes) or on request (diag `pairs`), by
+    // passes issued while other renders run; a pass issued alone (a lone frame) takes single
     // samples, whose shorter items end the launch sooner (config 3: 3.23-3.26 vs 3.38-3.45 ms),
-    // in a workspace of its own beside the ring. The wavefront variant stores single samples.
-    const bool pairs_ok = !wave && !(O.diag & RT_DIAG_NO_PAIRS);
+    // in a workspace of its own beside the ring. Culled LDS kernels only (the wavefront variant,
+    // brute force and the scalar-cache variant store single samples).
+    const bool pairs_ok = !wave && cull_mode == 7 && variant != rt::V_EXACT_SCALAR && !(O.diag & RT_DIAG_NO_PAIRS);
+    bool pairs = pairs_ok && (O.diag & RT_DIAG_PAIRS);
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     auto slot_rows = [&](uint64_t a, uint64_t b, bool pr) -> uint64_t {  // samples [a, b), a a multiple of 4
         const uint64_t nb = (std::min<uint64_t>(b, full_blocks_end) - std::min<uint64_t>(a, full_blocks_end)) / 4u;
@@ -773,7 +777,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // the ring's workspaces (pairs when there is a ring) and the lone passes' own one (singles)
     auto footprint = [&](uint32_t streams, uint32_t wsps, uint64_t sp) -> uint64_t {
         const uint64_t spe = std::min<uint64_t>(sp, P.spp);
-        const bool ring_pairs = pairs_ok && streams > 1;
+        const bool ring_pairs = pairs && streams > 1;
         const uint64_t dq = may_split ? deep_queue_bytes(n_pixels, n_pixels * spe) : 0u;
         uint64_t t = static_cast<uint64_t>(n_ws_of(streams, wsps)) * (ws_bytes(spe, ring_pairs) + dq);
         if (ring_pairs) t += ws_bytes(spe, false) + dq;
@@ -790,6 +794,10 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 wsps = 1;
                 continue;
             }
+            if (bufs > 1 && pairs_ok && !pairs) {
+                pairs = true;
+                continue;
+            }
             if (spp_pass > 4) {
                 spp_pass = std::max<uint64_t>(4, (std::min<uint64_t>(spp_pass, P.spp) - 1) & ~3ull);
                 continue;
@@ -804,7 +812,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     const bool pipe = bufs > 1;
     const uint32_t n_ws = n_ws_of(bufs, wsps);
     const uint64_t spe = std::min<uint64_t>(spp_pass, P.spp);
-    const bool ring_pairs = pairs_ok && pipe;
+    const bool ring_pairs = pairs && pipe;
     const uint32_t lone_ws = ring_pairs ? n_ws : kMaxWs;  // the lone passes' workspace (singles), if any
     auto ws_size = [&](uint32_t w) { return ws_bytes(spe, ring_pairs && w != lone_ws); };
     // under a cap, workspaces left larger (or more numerous) by earlier frames are re-cut once

@@ -554,8 +554,14 @@ __device__ __forceinline__ uint64_t min16_key(uint64_t k)
 // per-wave LDS of the transposed tests: the requesting rays by rank; a ray's minimum key comes
 // back in the last two words of its first record once its round is done (the round's rows read
 // their rays before any row writes a key, and later rounds read other rays)
+#ifndef RT_TKEY_SEPARATE
+#define RT_TKEY_SEPARATE 0  // A/B build switch: the rows' keys in an array of their own (512 B more per workgroup)
+#endif
 struct TransposeLds {
     float4 ray[kTransposeMax][2];   // {o.x, o.y, o.z | key lo, a | key hi}, {d.x, d.y, d.z, refined 1/a}
+#if RT_TKEY_SEPARATE
+    uint64_t key[kTransposeMax];
+#endif
 };
 template <bool FAST, bool STATS>
 __device__ __forceinline__ void members_transposed(const float4 *__restrict__ geo, const uint32_t *__restrict__ sidx,
@@ -616,16 +622,24 @@ __device__ __forceinline__ void members_transposed(const float4 *__restrict__ ge
         }
         key = min16_key(key);
         if (k == 0u && r < m) {
+#if RT_TKEY_SEPARATE
+            tw->key[r] = key;
+#else
             tw->ray[r][0].z = __uint_as_float((uint32_t)key);
             tw->ray[r][0].w = __uint_as_float((uint32_t)(key >> 32));
+#endif
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (req) {
+#if RT_TKEY_SEPARATE
+        const uint64_t kk = tw->key[rank];
+#else
         const float4 q = tw->ray[rank][0];
         const uint64_t kk = ((uint64_t)__float_as_uint(q.w) << 32) | __float_as_uint(q.z);
+#endif
         if (kk < h.key) h.key = kk;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -854,7 +868,9 @@ constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_
 // instantiation, render_deep_kernel, so neither launch carries the other's code.
 // WPB: waves per workgroup (4; the lone deep launch 8, which shares one LDS copy of the scene
 // between twice the waves)
-template <int V, int CULL, bool STATS, bool COUNT, bool DEEP, int WPB>
+// PAIRS: the main launch of a pass that stores sample pairs (KParams::n_pair_items != 0,
+// DESIGN.md §4.2), its own instantiation: the pair bookkeeping costs the loop ~3% of its issue
+template <int V, int CULL, bool STATS, bool COUNT, bool DEEP, int WPB, bool PAIRS>
 __device__ __forceinline__ void render_body(const KParams &p)
 {
     constexpr bool FAST = (V == V_FAST_LDS);
@@ -898,7 +914,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
     // sample pairs, per lane (structure of arrays): the main launch parks a pair's first colour
     // here while the lane traces the second (or, in word 0, the first's deep-queue index when it
     // went to the queue); the deep launch keeps the path's own queue index in word 0
-    __shared__ float lds_park[3][64 * WPB];
+    // (three words per lane for the pair's parked colour; one, the queue index, in the deep launch)
+    __shared__ float lds_park[PAIRS ? 3 : 1][64 * WPB];
+    auto park = [&](int c, uint32_t sl) -> float & { return lds_park[PAIRS ? c : 0][sl]; };
     const uint32_t wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
 
     // the deep launch's waves issue ahead of other launches' waves (KParams::deep_prio): each of
@@ -1112,7 +1130,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
         }
 
         // a pair whose first sample ended last iteration: its second sample starts now
-        if (!DEEP && (it & kItRestart)) {
+        if (!DEEP && PAIRS && (it & kItRestart)) {
             fresh = true;
             it &= ~kItRestart;
         }
@@ -1127,10 +1145,11 @@ __device__ __forceinline__ void render_body(const KParams &p)
         // the pixel (enumeration index) and the sample of the pass of the lane's item word
         auto item_pixel = [&](uint32_t &s) -> uint32_t {
             const uint32_t sl = it & kItSlot;
-            const bool pr = sl < P.n_pair_items;
-            const uint32_t J = pr ? sl : sl - P.n_pair_items;
+            const uint32_t npi = PAIRS ? (uint32_t)P.n_pair_items : 0u;
+            const bool pr = sl < npi;
+            const uint32_t J = pr ? sl : sl - npi;
             const uint32_t q = udiv(J, fc->div_n_pixels);
-            s = pr ? 2u * q + (it >> 31) : 2u * fc->n_pairs + q;
+            s = !PAIRS ? q : pr ? 2u * q + (it >> 31) : 2u * fc->n_pairs + q;
             return J - q * fc->n_pixels;
         };
         auto finish = [&](f3 col) -> bool {
@@ -1167,17 +1186,17 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 }
             } else {
                 const uint32_t slot = it & kItSlot;
-                if (slot < P.n_pair_items) {
+                if (PAIRS && slot < P.n_pair_items) {
                     const uint32_t sl = thread_slot(wave_base);
                     if (!(it & kItSecond)) {
-                        lds_park[0][sl] = col.x;
-                        lds_park[1][sl] = col.y;
-                        lds_park[2][sl] = col.z;
+                        park(0, sl) = col.x;
+                        park(1, sl) = col.y;
+                        park(2, sl) = col.z;
                         it |= kItSecond | kItRestart;
                         return true;
                     }
                     // the first's colour, unless it went to the deep queue (which then adds this one)
-                    if (!(it & kItFirstDeep)) col = mk(lds_park[0][sl], lds_park[1][sl], lds_park[2][sl]) + col;  // RN(c_2j + c_2j+1)
+                    if (!(it & kItFirstDeep)) col = mk(park(0, sl), park(1, sl), park(2, sl)) + col;  // RN(c_2j + c_2j+1)
                 }
                 dst = P.slots + (size_t)checked<STATS>(slot, P.n_items, BC_SLOT, p.dbg) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
             }
@@ -1327,7 +1346,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     // the path's slot and pair link (rt_device.h kRole*)
                     const uint32_t slot = it & kItSlot, sl = thread_slot(wave_base);
                     uint32_t link = kRoleSingle << 30;
-                    if (slot >= P.n_pair_items) {
+                    if (!PAIRS || slot >= P.n_pair_items) {
                         alive = false;
                     } else {
                         link = kRolePartnerDone << 30;
@@ -1344,9 +1363,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
                                 P.deep.link[j1] = (kRoleBothFirst << 30) | j;
                             } else {  // the first's colour, parked in the lane's LDS words, to the slot
                                 float *dst = P.slots + (size_t)checked<STATS>(slot, P.n_items, BC_SLOT, p.dbg) * 3u;
-                                dst[0] = lds_park[0][sl];
-                                dst[1] = lds_park[1][sl];
-                                dst[2] = lds_park[2][sl];
+                                dst[0] = park(0, sl);
+                                dst[1] = park(1, sl);
+                                dst[2] = park(2, sl);
                             }
                             alive = false;
                         }
@@ -1579,17 +1598,17 @@ __device__ __forceinline__ void render_body(const KParams &p)
     }
 }
 
-template <int V, int CULL, bool STATS, bool COUNT>
+template <int V, int CULL, bool STATS, bool COUNT, bool PAIRS = false>
 __global__ __launch_bounds__(256, (kMinWaves<V, CULL, STATS>)) void render_kernel(const KParams p)
 {
-    render_body<V, CULL, STATS, COUNT, false, 4>(p);
+    render_body<V, CULL, STATS, COUNT, false, 4, PAIRS>(p);
 }
 // the deep launch of a split pass (culled scenes only); WPB = 8: the lone deep launch with the
 // shading records in LDS, whose workgroups per CU the LDS bounds
 template <int V, bool STATS, bool COUNT, int WPB>
 __global__ __launch_bounds__(64 * WPB, (WPB == 8 && !STATS ? RT_DEEP_WIDE_WAVES : kMinWaves<V, 7, STATS>)) void render_deep_kernel(const KParams p)
 {
-    render_body<V, 7, STATS, COUNT, true, WPB>(p);
+    render_body<V, 7, STATS, COUNT, true, WPB, false>(p);
 }
 
 // ---- the reference's CUDA variant (RT_FLAG_CUDA_COMPAT) -----------------------------------
@@ -2074,26 +2093,28 @@ __global__ __launch_bounds__(256, 6) void wave_bounce_kernel(const KWave w)
 // cull: 0 = brute force (every sphere, index order), 7 = two-level cluster walk with
 // transposed member tests (the default)
 // COUNT: the instantiation that tallies segments and tests (when the caller passes counters)
-template <int V, bool STATS, bool COUNT> static const void *ptr_cull(int cull)
+// pairs: the pass stores sample pairs (culled scenes only)
+template <int V, bool STATS, bool COUNT> static const void *ptr_cull(int cull, bool pairs)
 {
-    if (cull == 7) return reinterpret_cast<const void *>(&render_kernel<V, 7, STATS, COUNT>);
-    return reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, COUNT>);
+    if (cull == 7) return pairs ? reinterpret_cast<const void *>(&render_kernel<V, 7, STATS, COUNT, true>)
+                                : reinterpret_cast<const void *>(&render_kernel<V, 7, STATS, COUNT>);
+    return pairs ? nullptr : reinterpret_cast<const void *>(&render_kernel<V, 0, STATS, COUNT>);
 }
 
-template <bool COUNT> static const void *render_ptr_c(int variant, int cull)
+template <bool COUNT> static const void *render_ptr_c(int variant, int cull, bool pairs)
 {
     switch (variant) {
-    case V_EXACT_LDS: return ptr_cull<V_EXACT_LDS, false, COUNT>(cull);
-    case V_FAST_LDS: return ptr_cull<V_FAST_LDS, false, COUNT>(cull);
+    case V_EXACT_LDS: return ptr_cull<V_EXACT_LDS, false, COUNT>(cull, pairs);
+    case V_FAST_LDS: return ptr_cull<V_FAST_LDS, false, COUNT>(cull, pairs);
     case V_EXACT_SCALAR:
-        return cull ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false, COUNT>);
-    case V_STATS_LDS: return ptr_cull<V_EXACT_LDS, true, true>(cull);
+        return cull || pairs ? nullptr : reinterpret_cast<const void *>(&render_kernel<V_EXACT_SCALAR, 0, false, COUNT>);
+    case V_STATS_LDS: return ptr_cull<V_EXACT_LDS, true, true>(cull, pairs);
     default: return nullptr;
     }
 }
-static const void *render_ptr(int variant, int cull, bool count)
+static const void *render_ptr(int variant, int cull, bool count, bool pairs = false)
 {
-    return count ? render_ptr_c<true>(variant, cull) : render_ptr_c<false>(variant, cull);
+    return count ? render_ptr_c<true>(variant, cull, pairs) : render_ptr_c<false>(variant, cull, pairs);
 }
 
 template <bool COUNT, int WPB> static const void *render_deep_ptr_w(int variant)
@@ -2117,7 +2138,7 @@ hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid,
     // the deep launch (deep_mode != 0) exists for culled scenes only; only it has 8-wave groups
     const bool count = p.segments != nullptr;
     const void *fn = p.deep_mode ? (cull == 7 ? render_deep_ptr(variant, count, wpb) : nullptr)
-                                 : (wpb == 4 ? render_ptr(variant, cull, count) : nullptr);
+                                 : (wpb == 4 ? render_ptr(variant, cull, count, p.n_pair_items != 0) : nullptr);
     if (!fn) return hipErrorInvalidValue;
     const size_t lds = (size_t)p.lds_units * 16u;
     void *args[] = {const_cast<KParams *>(&p)};

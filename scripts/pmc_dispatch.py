@@ -22,7 +22,7 @@ a = ap.parse_args()
 def wanted(name):
     if "render_kernel" not in name and "render_deep_kernel" not in name:
         return False
-    return not a.timed or "<0, 7, false, false>" in name or "render_deep_kernel<0, false, false" in name
+    return not a.timed or "<0, 7, false, false, false>" in name or "render_deep_kernel<0, false, false" in name
 
 groups = {"main": defaultdict(list), "deep": defaultdict(list)}
 for d in sorted(x for x in glob.glob(os.path.join(a.root, "p*")) if os.path.isdir(x)):

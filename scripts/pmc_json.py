@@ -2,7 +2,7 @@
 """Condense rocprofv3 --pmc passes of bench.py into the JSON bench.py reads for roofline.traffic.
 
     python scripts/pmc_json.py <pmc dir with p*/run_counter_collection.csv> <out.json> \
-        [--kernel 'render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false, 4|8>'] [--config c3]
+        [--kernel 'render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8>'] [--config c3]
 
 Per frame (the kernel's dispatches of a frame summed, mean over frames and passes):
   hbm_bytes_per_frame  = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE counts half of the
@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ap = argparse.ArgumentParser()
 ap.add_argument("root")
 ap.add_argument("out")
-ap.add_argument("--kernel", default="render_kernel<0, 7, false, false> + render_deep_kernel<0, false, false, 4|8>",
+ap.add_argument("--kernel", default="render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8>",
                 help="kernel names joined by ' + '; the first one's dispatches count the frames")
 ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")

@@ -387,12 +387,12 @@ def test_sample_pairs_through_the_deep_queue(streams, opts):
     (pairs and single tail samples, several passes) follow each other on one scene, so every
     workspace's deep queue is laid out anew between passes (its pair-arrival words must start at
     zero); one workspace (render_streams = 1) or the default rotation. Each frame equals the
-    oracle bit for bit, as does the unpaired render (no_pairs)."""
+    oracle bit for bit, as does the unpaired render (the default without a workspace cap)."""
     torch = pytest.importorskip("torch")
     s, m = _glass_scene_frames()
     # one pass budget for the scene (8 samples of the largest frame): the frames below are cut
     # into passes of different sizes, single tail samples included
-    opts.set(deep_min_items=0, deep_split=1, render_streams=streams, max_pass_bytes=80 * 44 * 12 * 8)
+    opts.set(deep_min_items=0, deep_split=1, render_streams=streams, max_pass_bytes=80 * 44 * 12 * 8, pairs=True)
     cases = [(64, 40, 10), (48, 30, 23), (80, 44, 16), (40, 24, 7), (64, 40, 10), (80, 44, 26)]
     ds = rt.DeviceScene((s, m))
     stream = torch.cuda.current_stream().cuda_stream
@@ -406,11 +406,11 @@ def test_sample_pairs_through_the_deep_queue(streams, opts):
     for (W, H, spp), o in zip(cases, outs):
         want, _ = O.render_f32(s, m, O.camera_default(W, H), rt.make_params(W, H, spp, 64, 31))
         _bits_equal(o.cpu().numpy(), want, f"{W}x{H} spp {spp}")
-    opts.set(no_pairs=True)
+    opts.set(pairs=False)
     W, H, spp = cases[1]
     img, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 31))
     want, _ = O.render_f32(s, m, O.camera_default(W, H), rt.make_params(W, H, spp, 64, 31))
-    _bits_equal(img, want, "no_pairs")
+    _bits_equal(img, want, "singles")
 
 
 def _glass_scene_frames():
@@ -558,8 +558,8 @@ def test_multi_context_rccl_branch_with_standin_transport(n):
 
 # ---- a bounded HBM footprint (rt_options.max_workspace_bytes) ------------------------------
 def test_workspace_cap_bounds_memory_with_the_same_bits(opts):
-    """Under max_workspace_bytes the library cuts a frame into smaller passes, then fewer
-    workspaces per stream, then fewer streams: the scene's workspaces stay within the cap
+    """Under max_workspace_bytes the library takes one workspace per stream, then sample pairs
+    (half the slot bytes), then smaller passes, then fewer streams: the scene's workspaces stay within the cap
     (rt_scene_usage_get), frames streamed without host sync keep the uncapped bits and segment
     counts, and a cap below one 4-sample pass is RT_ERR_CAPACITY."""
     torch = pytest.importorskip("torch")

@@ -32,7 +32,7 @@ namespace rt {
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream, int wpb = 4);
 hipError_t deep_occupancy(int variant, int wpb, size_t lds, int *blocks_per_cu, size_t *static_lds);
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
-hipError_t static_lds_render(int variant, int cull, size_t *bytes);
+hipError_t static_lds_render(int variant, int cull, size_t *bytes, bool pairs = false);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream);
 hipError_t launch_wave_gen(const KWave &w, hipStream_t stream);
@@ -183,6 +183,7 @@ struct rt_scene {
     // static LDS of the render kernel per traversal, [0] brute force, [1] culled (per-wave
     // transposed-test records and per-lane arrays; hipFuncGetAttributes)
     size_t static_lds[2] = {0, 0};
+    size_t static_lds_pairs = 0;  // the culled kernel's sample-pair instantiation (its parked colours)
     // the last render's cut (rt_scene_usage_get)
     uint32_t used_streams = 0, used_ws = 0, used_pass = 0, used_deep = 0;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
@@ -521,6 +522,7 @@ int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_ma
     if (rc == RT_OK) {
         hipError_t e = rt::static_lds_render(rt::V_EXACT_LDS, 0, &sc->static_lds[0]);
         if (e == hipSuccess) e = rt::static_lds_render(rt::V_EXACT_LDS, 7, &sc->static_lds[1]);
+        if (e == hipSuccess) e = rt::static_lds_render(rt::V_EXACT_LDS, 7, &sc->static_lds_pairs, true);
         if (e != hipSuccess) rc = fail(RT_ERR_DEVICE, std::string("hipFuncGetAttributes: ") + hipGetErrorString(e));
     }
     for (uint32_t i = 0; rc == RT_OK && i < rt_scene::kRing; ++i) {
@@ -749,7 +751,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // samples, whose shorter items end the launch sooner (config 3: 3.23-3.26 vs 3.38-3.45 ms),
     // in a workspace of its own beside the ring. Culled LDS kernels only (the wavefront variant,
     // brute force and the scalar-cache variant store single samples).
-    const bool pairs_ok = !wave && cull_mode == 7 && variant != rt::V_EXACT_SCALAR && !(O.diag & RT_DIAG_NO_PAIRS);
+    const bool pairs_ok = !wave && cull_mode == 7 && variant != rt::V_EXACT_SCALAR && !(O.diag & RT_DIAG_NO_PAIRS) &&
+                          lds + sc->static_lds_pairs <= sc->max_lds;
     bool pairs = pairs_ok && (O.diag & RT_DIAG_PAIRS);
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     auto slot_rows = [&](uint64_t a, uint64_t b, bool pr) -> uint64_t {  // samples [a, b), a a multiple of 4

@@ -860,6 +860,9 @@ __device__ __forceinline__ float4 dielectric_record(const KP &P, const float4 *b
 template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_PER_SIMD;
 // the lone deep kernel's occupancy bound (waves per SIMD; 6: 3 workgroups of 8 waves per CU)
+#ifndef RT_DEEP_HOIST
+#define RT_DEEP_HOIST 0  // A/B build switch: the lone deep kernel keeps its parameters in registers
+#endif
 #ifndef RT_DEEP_WIDE_WAVES
 #define RT_DEEP_WIDE_WAVES 6
 #endif
@@ -991,11 +994,17 @@ __device__ __forceinline__ void render_body(const KParams &p)
         }
 #endif
         fc_ptr_t fc = fc_base;
+#if RT_DEEP_HOIST
+        if (!(DEEP && WPB == 8))
+#endif
         asm volatile("" : "+s"(fc));
         // the kernel parameters, re-read from the kernarg segment each iteration through an
         // opaque pointer: their uses (the deep split, the shading records, the refill) then
         // hold no SGPRs across the loop (31 SGPRs were spilled to VGPR lanes otherwise)
         kp_ptr_t kpp = kp_base;
+#if RT_DEEP_HOIST
+        if (!(DEEP && WPB == 8))
+#endif
         asm volatile("" : "+s"(kpp));
         const __attribute__((address_space(4))) KParams &P = *kpp;
         // ---- refill items for idle lanes and start their samples -------------------
@@ -2165,9 +2174,9 @@ hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t ld
 }
 
 // the static LDS of a render kernel (per-wave and per-lane arrays; the scene blob comes on top)
-hipError_t static_lds_render(int variant, int cull, size_t *bytes)
+hipError_t static_lds_render(int variant, int cull, size_t *bytes, bool pairs)
 {
-    const void *fn = render_ptr(variant, cull, false);
+    const void *fn = render_ptr(variant, cull, false, pairs);
     if (!fn) return hipErrorInvalidValue;
     hipFuncAttributes a{};
     const hipError_t e = hipFuncGetAttributes(&a, fn);

@@ -30,6 +30,9 @@ using namespace rthost;
 
 namespace rt {
 hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid, hipStream_t stream, int wpb = 4);
+#ifndef RT_LONE_DEEP_TMAX
+#define RT_LONE_DEEP_TMAX 4u  // the lone deep launch's transposition threshold (below)
+#endif
 hipError_t deep_occupancy(int variant, int wpb, size_t lds, int *blocks_per_cu, size_t *static_lds);
 hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
 hipError_t static_lds_render(int variant, int cull, size_t *bytes, bool pairs = false);
@@ -1022,6 +1025,12 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                         wpb = 8;
                         dgrid = static_cast<uint32_t>(ow * sc->cu_count);
                         kd.deep_static = RT_DEEP_STATIC ? 1u : 0u;
+                        // its waves run alone on their SIMDs, so a cluster's transposed member
+                        // test (three LDS round trips) pays off for fewer requesting lanes: at
+                        // most 4 here (lone deep launch 0.351-0.360 vs 0.370-0.377 ms at 16;
+                        // 1-8 alike, per-lane tests always 0.400-0.405; profiles/r05/deep/
+                        // lone_deep_tmax.txt)
+                        kd.transpose_max = std::min<uint32_t>(O.transpose_max, RT_LONE_DEEP_TMAX);
                     }
                 }
                 if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) {

@@ -861,7 +861,9 @@ template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_PER_SIMD;
 // the lone deep kernel's occupancy bound (waves per SIMD; 6: 3 workgroups of 8 waves per CU)
 #ifndef RT_DEEP_HOIST
-#define RT_DEEP_HOIST 0  // A/B build switch: the lone deep kernel keeps its parameters in registers
+// the lone deep kernel keeps its parameters in registers (106 SGPRs, no spills at its 6-wave bound;
+// lone deep launch 0.341-0.351 vs 0.351-0.360 ms re-reading them, profiles/r05/deep/lone_deep_tmax.txt)
+#define RT_DEEP_HOIST 1
 #endif
 #ifndef RT_DEEP_WIDE_WAVES
 #define RT_DEEP_WIDE_WAVES 6

@@ -313,7 +313,8 @@ int rt_scene_debug_counters(rt_scene *scene, uint64_t out[16], int reset);
 /* Diagnostics: per-wave records of the last instrumented render launch, out[4w .. 4w+3] for
  * wave w of the grid = {time the wave found every queue dry, exit} (100 MHz realtime
  * clock), (shader-clock cycles in the loop << 32 | refill rounds << 16 | loop iterations),
- * and (hardware CU id << 48 | iterations after dry << 32 | low 32 bits of the wave's start on
+ * and (hardware CU id << 48 | iterations after dry (a deep launch: iterations in which the wave
+ * walked the clusters) << 32 | low 32 bits of the wave's start on
  * the realtime clock); at most max_waves records, *n = records written (0 without
  * RT_DIAG_STATS).                                                                            */
 int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, uint32_t *n);

@@ -1019,7 +1019,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                         // against the 4-wave deep kernel it replaces, with the same blob in LDS
                         // (the main kernel's occupancy stood in for it)
                         RT_HIP(rt::deep_occupancy(variant, 4, bytes, &o4, &st4));
-                        ow = bytes + st8 <= sc->max_lds && o8 * 8 > o4 * 4 ? o8 : 0;
+                        // (the instrumented kernel follows the product's choice: wide whenever it fits)
+                        ow = bytes + st8 <= sc->max_lds && (o8 * 8 > o4 * 4 || (variant == rt::V_STATS_LDS && o8 > 0)) ? o8 : 0;
                     }
                     if (RT_DEEP_WIDE && ow > 0) {
                         wpb = 8;

@@ -723,7 +723,7 @@ __device__ __forceinline__ uint64_t sphere_key(bool want, float4 s, uint32_t id,
 // The neighbour slots of a lane that does not test a neighbour are 0, not its word's: a lane's
 // word may be stale (left by an earlier path) or, before the lane's first dielectric hit, whatever
 // the LDS held — bounded by that lane's own `skip` since fd383c3. The instrumented kernel (STATS)
-// checks the slot against n_geo, starts every lane's word at 0x7fff7fff (slots past any blob), and
+// checks the slot against n_geo, starts every lane's word at 0x3fffffff (slots past any blob, no list), and
 // with `unbounded` (KParams::diag_unbounded_nb) forms it the old way, so the check fires
 // (tests/test_gpu_parity.py test_neighbour_slots_are_bounded).
 template <bool FAST, bool STATS>
@@ -860,6 +860,9 @@ __device__ __forceinline__ float4 dielectric_record(const KP &P, const float4 *b
 template <int V, int CULL, bool STATS>
 constexpr int kMinWaves = (CULL == 7 && !STATS) ? RT_CULL7_WAVES : RT_MIN_WAVES_PER_SIMD;
 // the lone deep kernel's occupancy bound (waves per SIMD; 6: 3 workgroups of 8 waves per CU)
+#ifndef RT_DEEP_REGHINT
+#define RT_DEEP_REGHINT 0
+#endif
 #ifndef RT_DEEP_HOIST
 // the lone deep kernel keeps its parameters in registers (106 SGPRs, no spills at its 6-wave bound;
 // lone deep launch 0.341-0.351 vs 0.351-0.360 ms re-reading them, profiles/r05/deep/lone_deep_tmax.txt)
@@ -916,6 +919,13 @@ __device__ __forceinline__ void render_body(const KParams &p)
     __shared__ float4 lds_pn[64 * WPB];
     __shared__ uint32_t lds_hid[64 * WPB];
     __shared__ uint32_t lds_nb[64 * WPB];  // the dielectric sphere's shortcut word (hint_candidate)
+    // (the lone deep kernel keeps the three in registers: RT_DEEP_REGHINT, an A/B build switch)
+    constexpr bool kRegHint = DEEP && WPB == 8 && RT_DEEP_REGHINT;
+    uint32_t r_hid = ~0u, r_nb = 0u;
+    float4 r_pn = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto HID = [&](uint32_t sl) -> uint32_t & { if constexpr (kRegHint) return r_hid; else return lds_hid[sl]; };
+    auto NB = [&](uint32_t sl) -> uint32_t & { if constexpr (kRegHint) return r_nb; else return lds_nb[sl]; };
+    auto PN = [&](uint32_t sl) -> float4 & { if constexpr (kRegHint) return r_pn; else return lds_pn[sl]; };
     // sample pairs, per lane (structure of arrays): the main launch parks a pair's first colour
     // here while the lane traces the second (or, in word 0, the first's deep-queue index when it
     // went to the queue); the deep launch keeps the path's own queue index in word 0
@@ -951,15 +961,15 @@ __device__ __forceinline__ void render_body(const KParams &p)
     // a fresh sample whose lens draw did not finish within RT_REJECT_CAP attempts: its camera
     // stream state waits in (o.x, o.y) and its jittered (u, v) in (d.x, d.y) until it does
     bool pend_lens = false;
-    // lds_hid[lane] != ~0: the lane's last hit was a dielectric sphere, tested first next segment
+    // HID(lane) != ~0: the lane's last hit was a dielectric sphere, tested first next segment
     // (hint_candidate); kept in LDS, not in a register (at 72 VGPRs one more value spills)
-    lds_hid[thread_slot(wave_base)] = ~0u;
+    HID(thread_slot(wave_base)) = ~0u;
     // the instrumented kernel: neighbour words that no dielectric hit wrote point past any blob
     // (hint_candidate's bounds check)
-    if (STATS) lds_nb[thread_slot(wave_base)] = 0x7fff7fffu;
+    if (STATS) NB(thread_slot(wave_base)) = 0x3fffffffu;
     WaveTally<COUNT> wt;
     Dbg dbg{};
-    uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0, dbg_dealt = 0;
+    uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0, dbg_dealt = 0, dbg_walks = 0;
     uint64_t t_dry = 0;  // STATS: realtime when this wave found every queue empty
     // STATS build only: shader-clock cycles per loop region, summed over the wave's iterations
     uint64_t cyc[5] = {0, 0, 0, 0, 0};  // refill, sample start, closest hit, shading, fold
@@ -1125,10 +1135,10 @@ __device__ __forceinline__ void render_body(const KParams &p)
                             sf = gld4(P.blob + P.shade_offset, 2u * ib);
                             dr = gld4(P.blob, di);
                         }
-                        lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);
-                        lds_nb[sl] = __float_as_uint(dr.w);
+                        PN(sl) = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);
+                        NB(sl) = __float_as_uint(dr.w);
                     }
-                    lds_hid[sl] = hid;
+                    HID(sl) = hid;
                 } else {
                     it = I;  // a pair item (the pass's full blocks) or a single tail sample; its slot
                     alive = fresh = true;
@@ -1249,7 +1259,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
             }
             att = mk(1.f, 1.f, 1.f);
             depth = 0;
-            lds_hid[thread_slot(wave_base)] = ~0u;
+            HID(thread_slot(wave_base)) = ~0u;
         }
         // ---- one rejection loop for the wave (raytracer.hxx:32-43) ------------------------
         // Fresh lanes draw the lens offset from their camera stream (camera.hxx:52); lanes
@@ -1302,7 +1312,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 if (!pend_metal) {
                     d = (d + r) - o;                       // lambert :135, d held p + n, o = p
                 } else {
-                    const float4 pn = lds_pn[thread_slot(wave_base)];
+                    const float4 pn = PN(thread_slot(wave_base));
                     const f3 nd = d + r * pn.w;            // metal :147, d held reflect(unit(d), n)
                     if (dot(nd, mk(pn.x, pn.y, pn.z)) > 0.f) {
                         d = nd;
@@ -1338,7 +1348,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
             if (ballot(dv)) {
                 uint32_t j = ~0u, r = 0;
                 if (dv) {
-                    const uint32_t hid = lds_hid[thread_slot(wave_base)];
+                    const uint32_t hid = HID(thread_slot(wave_base));
                     r = hid != ~0u ? (hid & 7u) : (blockIdx.x & 7u);
                     j = atomicAdd(P.deep.ctr + r * kQueueStride + kDeepCount, 1u);
                 }
@@ -1352,7 +1362,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     f[3 * cap + j] = d.x; f[4 * cap + j] = d.y; f[5 * cap + j] = d.z;
                     f[6 * cap + j] = att.x; f[7 * cap + j] = att.y; f[8 * cap + j] = att.z;
                     P.deep.rng[j] = rng;
-                    P.deep.hid[j] = lds_hid[thread_slot(wave_base)];
+                    P.deep.hid[j] = HID(thread_slot(wave_base));
                     P.deep.px[px] = 1;
                     // the path's slot and pair link (rt_device.h kRole*)
                     const uint32_t slot = it & kItSlot, sl = thread_slot(wave_base);
@@ -1417,9 +1427,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
             uint64_t key0 = no_hit();
             bool skip = false;
             const uint32_t sl = thread_slot(wave_base);
-            const uint32_t hid = lds_hid[sl];
+            const uint32_t hid = HID(sl);
             if (ballot(seg && hid != ~0u))
-                key0 = hint_candidate<FAST, STATS>(seg && hid != ~0u, lds_pn[sl], hid, lds_nb[sl], geo, sidx, o, d, rd, P.iso,
+                key0 = hint_candidate<FAST, STATS>(seg && hid != ~0u, PN(sl), hid, NB(sl), geo, sidx, o, d, rd, P.iso,
                                                    skip, P.n_geo, P.diag_unbounded_nb, p.dbg);
             const bool walk = seg && !skip;
             const uint64_t wm = ballot(walk);
@@ -1427,6 +1437,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 dbg.ev[EV_ISO_LANES] += (uint32_t)__popcll(segm & ~wm);
                 if (segm && !wm) ++dbg.ev[EV_WALK_SKIPPED];
             }
+            if (STATS && lane == 0 && wm) ++dbg_walks;  // iterations in which the wave walked
             h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
@@ -1502,7 +1513,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     att = att * mk(md.x, md.y, md.z);           // main.cxx:65 (unused if absorbed)
                     // raytracer.hxx:120-199
                     o = hp;
-                    if (kind != 2u) lds_hid[thread_slot(wave_base)] = ~0u;  // no hint after lambert, metal
+                    if (kind != 2u) HID(thread_slot(wave_base)) = ~0u;  // no hint after lambert, metal
                     if (kind == 0u) {                           // lambert, :132-141
                         RT_EV(EV_LAMBERT);
                         d = hp + hn;                            // + rius next iteration, then - p
@@ -1522,7 +1533,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                         const f3 rf = reflect(ud, hn);
                         if (kind == 1u) {                       // metal, :143-156
                             d = rf;                             // + rius * roughness next iteration
-                            lds_pn[thread_slot(wave_base)] = make_float4(hn.x, hn.y, hn.z, md.w);
+                            PN(thread_slot(wave_base)) = make_float4(hn.x, hn.y, hn.z, md.w);
                             pend = true;
                             pend_metal = true;
                         } else {                                // dielectric, :158-194
@@ -1531,10 +1542,10 @@ __device__ __forceinline__ void render_body(const KParams &p)
                             const float4 dcs = dielectric_record<V>(P, blob, ib);
                             {   // the next segment tests this sphere first (hint_candidate)
                                 const uint32_t sl = thread_slot(wave_base);
-                                lds_pn[sl] = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);  // its geo entry, raytracer.hxx:58
+                                PN(sl) = make_float4(sf.x, sf.y, sf.z, sf.w * sf.w);  // its geo entry, raytracer.hxx:58
                                 const uint32_t w = __float_as_uint(dcs.w);  // its shortcut word
-                                lds_hid[sl] = ib | (w & kShortcut);
-                                lds_nb[sl] = w;
+                                HID(sl) = ib | (w & kShortcut);
+                                NB(sl) = w;
                             }
                             f3 outward = mk(-hn.x, -hn.y, -hn.z);
                             float ri = md.w, xs = dcs.y;
@@ -1604,7 +1615,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
             p.dbg[17 + 4 * w] = __builtin_amdgcn_s_memrealtime();
             p.dbg[18 + 4 * w] = (min(cy, 0xffffffffull) << 32) | (min(dbg_refills, 65535u) << 16) | min(dbg_iters, 65535u);
             p.dbg[19 + 4 * w] = ((unsigned long long)(__smid() & 0xffffu) << 48) |
-                                ((unsigned long long)min(dbg_iters_dry, 65535u) << 32) | (uint32_t)t_wave0;
+                                ((unsigned long long)min(DEEP ? dbg_walks : dbg_iters_dry, 65535u) << 32) | (uint32_t)t_wave0;
         }
     }
 }

@@ -253,7 +253,8 @@ class DeviceScene:
         return dict(zip(self.EVENTS, list(buf)))
 
     def debug_timeline(self, max_waves=65536):
-        """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry, start, cycles) of the
+        """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry (the deep launch:
+        iterations in which the wave walked the clusters), start, cycles) of the
         last instrumented launch (options stats=True; dry = when the wave found every queue empty;
         times in ticks of the 100 MHz clock; cycles = shader-clock cycles in the loop, so
         cycles / (exit - start) x 100 MHz is the clock the wave ran at), see rt_scene_debug_timeline."""

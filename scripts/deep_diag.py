@@ -69,6 +69,18 @@ for text in a.options:
            "iters_per_busy_wave": {f"p{int(f * 100)}": (sorted(r[2] for r in busy)[min(len(busy) - 1, int(f * len(busy)))] if busy else None)
                                    for f in (0.0, 0.5, 0.9, 1.0)}}
     res["paths_dealt"] = c.get("items_dealt", 0)
+    res["deep_launch"] = ds.usage().get("deep_launch")
+    # per busy wave: life (us), iterations, iterations in which it walked; the slowest and fastest tenth
+    life = sorted(((r[1] - r[6]) / 100.0, r[2], r[5]) for r in busy)
+    if life:
+        k = max(1, len(life) // 10)
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        res["fastest_tenth"] = {"life_us": med([x[0] for x in life[:k]]), "iters": med([x[1] for x in life[:k]]),
+                                "walk_iters": med([x[2] for x in life[:k]])}
+        res["slowest_tenth"] = {"life_us": med([x[0] for x in life[-k:]]), "iters": med([x[1] for x in life[-k:]]),
+                                "walk_iters": med([x[2] for x in life[-k:]])}
+        res["walk_iters_per_busy_wave"] = {f"p{int(f * 100)}": sorted(x[2] for x in life)[min(len(life) - 1, int(f * len(life)))]
+                                           for f in (0.0, 0.5, 0.9, 1.0)}
     res["segments"] = c["segments"]
     its = sorted(r[2] for r in busy)
     hist = {}

@@ -95,7 +95,7 @@ def test_bounds_checked_frame_stream_c3():
     """Round 4's hipErrorIllegalAddress, pinned. The instrumented kernel
     (options stats=True) checks every lane-computed index into the scene blob, the sample slots
     and the deep queue before it uses it, and starts every lane's walk-shortcut neighbour word
-    at 0x7fff7fff (slots past any blob), as a stale or never-written word may hold. Over the
+    at 0x3fffffff (slots past any blob), as a stale or never-written word may hold. Over the
     config-3 frame stream (a lone first frame with its 8-wave deep launch, then frames in flight
     with 4-wave deep launches and global shading records) no index passes its bound, and the
     frames equal the reference's. With unbounded_nb the neighbour slots are formed without the

@@ -991,6 +991,9 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 // the level-3 gate only costs there (alike within box noise, fewer box tests;
                 // same bits)
                 kd.use_root = 0u;
+#ifdef RT_DEEP_TMAX  // A/B build switch: every deep launch's transposition threshold
+                kd.transpose_max = std::min<uint32_t>(O.transpose_max, RT_DEEP_TMAX);
+#endif
                 // its waves at the top issue priority: each path is a chain of ~56 dependent
                 // iterations, and beside other renders' waves every iteration waits for the
                 // SIMD's other waves (config 3's 8-way share, split, 7 streams: 0.513-0.515 ms vs

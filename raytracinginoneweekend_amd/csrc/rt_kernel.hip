@@ -970,6 +970,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
     WaveTally<COUNT> wt;
     Dbg dbg{};
     uint32_t dbg_iters = 0, dbg_refills = 0, dbg_iters_dry = 0, dbg_dealt = 0, dbg_walks = 0;
+    uint32_t dbg_walks_nohint = 0;  // (deep launch) walks with a walking lane that has no hint sphere
     uint64_t t_dry = 0;  // STATS: realtime when this wave found every queue empty
     // STATS build only: shader-clock cycles per loop region, summed over the wave's iterations
     uint64_t cyc[5] = {0, 0, 0, 0, 0};  // refill, sample start, closest hit, shading, fold
@@ -1437,7 +1438,11 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 dbg.ev[EV_ISO_LANES] += (uint32_t)__popcll(segm & ~wm);
                 if (segm && !wm) ++dbg.ev[EV_WALK_SKIPPED];
             }
-            if (STATS && lane == 0 && wm) ++dbg_walks;  // iterations in which the wave walked
+            if (STATS) {
+                const uint64_t nh = ballot(walk && hid == ~0u);
+                if (lane == 0 && wm) ++dbg_walks;  // iterations in which the wave walked
+                if (lane == 0 && nh) ++dbg_walks_nohint;
+            }
             h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
@@ -1611,7 +1616,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
         const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (lane == 0 && w < kDbgWaves) {
             const unsigned long long cy = cyc[0] + cyc[1] + cyc[2] + cyc[3] + cyc[4];
-            p.dbg[16 + 4 * w] = t_dry ? t_dry : __builtin_amdgcn_s_memrealtime();
+            // (a deep launch: the walks with a lane that has no hint sphere << 32 | the walks)
+            p.dbg[16 + 4 * w] = DEEP ? ((unsigned long long)dbg_walks_nohint << 32 | dbg_walks)
+                                     : (t_dry ? t_dry : __builtin_amdgcn_s_memrealtime());
             p.dbg[17 + 4 * w] = __builtin_amdgcn_s_memrealtime();
             p.dbg[18 + 4 * w] = (min(cy, 0xffffffffull) << 32) | (min(dbg_refills, 65535u) << 16) | min(dbg_iters, 65535u);
             p.dbg[19 + 4 * w] = ((unsigned long long)(__smid() & 0xffffu) << 48) |

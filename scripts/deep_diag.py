@@ -79,6 +79,10 @@ for text in a.options:
                                 "walk_iters": med([x[2] for x in life[:k]])}
         res["slowest_tenth"] = {"life_us": med([x[0] for x in life[-k:]]), "iters": med([x[1] for x in life[-k:]]),
                                 "walk_iters": med([x[2] for x in life[-k:]])}
+        # record word 0 of a deep launch: walks with a hint-less walking lane << 32 | walks
+        nh = {id(r): (r[0] >> 32) for r in busy}
+        res["slowest_tenth"]["walks_with_hintless_lane"] = med([nh[id(r)] for r in sorted(busy, key=lambda r: r[1] - r[6])[-k:]])
+        res["fastest_tenth"]["walks_with_hintless_lane"] = med([nh[id(r)] for r in sorted(busy, key=lambda r: r[1] - r[6])[:k]])
         res["walk_iters_per_busy_wave"] = {f"p{int(f * 100)}": sorted(x[2] for x in life)[min(len(life) - 1, int(f * len(life)))]
                                            for f in (0.0, 0.5, 0.9, 1.0)}
     res["segments"] = c["segments"]

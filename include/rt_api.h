@@ -327,7 +327,7 @@ int rt_scene_debug_timeline(rt_scene *scene, uint64_t *out, uint32_t max_waves, 
  * direction (metal/dielectric), [18] dielectric, [19] sample stores, [20] metal absorptions,
  * [21] live lanes summed over iterations, [22] iterations after the item queues ran dry, [23]
  * live lanes summed over those, [24] lanes that skipped the walk (shortcut), [25] iterations
- * whose walk no lane needed.                                        */
+ * whose walk no lane needed, [26..29] iterations whose walk 1, 2, 3-4, 5-8 lanes needed.                                        */
 int rt_scene_debug_events(rt_scene *scene, uint64_t out[32], int reset);
 /* Enqueue the gamma/u8 epilogue over n_pixels RGB f32 texels.                          */
 int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixels,

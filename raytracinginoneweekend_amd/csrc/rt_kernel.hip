@@ -74,6 +74,7 @@ enum DbgEvent : uint32_t {
     EV_DRY_LANES,   // live lanes summed over those
     EV_ISO_LANES,   // lanes that skipped the cluster walk (isolated hint sphere), summed over iterations
     EV_WALK_SKIPPED,  // wave iterations with segments whose cluster walk no lane needed
+    EV_WALK1, EV_WALK2, EV_WALK4, EV_WALK8,  // wave iterations whose walk 1, 2, 3-4, 5-8 lanes need
     EV_COUNT
 };
 static_assert(EV_COUNT <= kDbgEvents, "event counters");
@@ -1437,6 +1438,11 @@ __device__ __forceinline__ void render_body(const KParams &p)
             if (STATS && first_active_lane()) {
                 dbg.ev[EV_ISO_LANES] += (uint32_t)__popcll(segm & ~wm);
                 if (segm && !wm) ++dbg.ev[EV_WALK_SKIPPED];
+                const uint32_t nw = (uint32_t)__popcll(wm);
+                if (nw == 1u) ++dbg.ev[EV_WALK1];
+                else if (nw == 2u) ++dbg.ev[EV_WALK2];
+                else if (nw >= 3u && nw <= 4u) ++dbg.ev[EV_WALK4];
+                else if (nw >= 5u && nw <= 8u) ++dbg.ev[EV_WALK8];
             }
             if (STATS) {
                 const uint64_t nh = ballot(walk && hid == ~0u);

@@ -244,7 +244,7 @@ class DeviceScene:
     EVENTS = ["iter", "refill_trip", "fresh", "reject_trip", "lens_done", "scatter_done", "root_gate_pass", "super",
               "super_pass", "cluster_req", "transposed", "t_round", "t_far", "per_lane_members", "sky", "hit",
               "lambert", "unit_dir", "dielectric", "store", "metal_absorb", "live_lanes", "dry_iter", "dry_lanes",
-              "iso_lanes", "walk_skipped"]
+              "iso_lanes", "walk_skipped", "walk_1", "walk_2", "walk_3_4", "walk_5_8"]
 
     def debug_events(self, reset=True):
         """Block-execution counts of the instrumented kernel (options stats=True), see rt_scene_debug_events."""

@@ -462,8 +462,9 @@ def main():
             if not rehearse:
                 gather(tile8 if rgb8 else tile)
             elif args.rehearse_gather:
-                for r in range(1, rehearse):  # one copy kernel per peer, as the gather's receives
-                    fake[r].copy_(tile)
+                # the peers' tiles landing in the gather buffer: one copy kernel, as RCCL's gather
+                # receives them in one grouped operation; then the de-interleave, as FrameGather
+                fake[1:].copy_(tile.unsqueeze(0).expand(rehearse - 1, *tile.shape))
                 frame_r.view(rows, rehearse, W, 3).copy_(fake.transpose(0, 1))
 
         for _ in range(warmup):

@@ -160,6 +160,12 @@ typedef struct rt_options {
                                        (ray, member) pairs over the wave, 0..16 (16)           */
     uint32_t wave_queue_rays;       /* RT_FLAG_WAVEFRONT: rays per chunk, >= 64 (2^25)        */
     uint32_t diag;                  /* rt_diag bits (0)                                        */
+    uint64_t ring_pass_bytes;       /* with frames in flight: slot workspace of a pass issued
+                                       beside other renders, 0 or 12 B .. 2 GiB (384 MiB); the
+                                       frame's samples are cut into equal passes of a multiple
+                                       of 4 within it, if they hold 32 samples or more. A frame
+                                       issued alone that fits max_pass_bytes runs in one pass in
+                                       a workspace of its own. 0 = passes of max_pass_bytes     */
 } rt_options;
 enum rt_diag {
     RT_DIAG_IEEE_ROOTS = 1u << 0,      /* the IEEE sqrt/division sequences for every root     */

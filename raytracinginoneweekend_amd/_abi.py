@@ -63,7 +63,7 @@ class RtOptions(C.Structure):
         ("size", C.c_uint32), ("render_streams", C.c_uint32), ("workspaces_per_stream", C.c_uint32),
         ("deep_split", C.c_uint32), ("max_pass_bytes", C.c_uint64), ("max_workspace_bytes", C.c_uint64),
         ("deep_min_items", C.c_uint64), ("cluster_size", C.c_uint32), ("transpose_max", C.c_uint32),
-        ("wave_queue_rays", C.c_uint32), ("diag", C.c_uint32),
+        ("wave_queue_rays", C.c_uint32), ("diag", C.c_uint32), ("ring_pass_bytes", C.c_uint64),
     ]
 
 
@@ -95,7 +95,7 @@ MATERIAL_DTYPE = np.dtype([("kind", "<u4"), ("albedo", "<f4", (3,)), ("param", "
 assert SPHERE_DTYPE.itemsize == C.sizeof(RtSphere) == 20
 assert MATERIAL_DTYPE.itemsize == C.sizeof(RtMaterial) == 20
 assert C.sizeof(RtParams) == 40
-assert C.sizeof(RtOptions) == 56 and C.sizeof(RtSceneUsage) == 40
+assert C.sizeof(RtOptions) == 64 and C.sizeof(RtSceneUsage) == 40
 
 
 def ptr(arr, ctype=C.c_void_p):

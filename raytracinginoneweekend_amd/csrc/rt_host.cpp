@@ -780,14 +780,38 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         return static_cast<uint32_t>(std::min<uint64_t>(n_pixels * std::min<uint64_t>(sp, P.spp), O.wave_queue_rays));
     };
     auto n_ws_of = [](uint32_t streams, uint32_t wsps) { return streams > 1 ? streams * wsps : 1u; };
-    // the ring's workspaces (pairs when there is a ring) and the lone passes' own one (singles)
+    // Ring passes (rt_options.ring_pass_bytes): with frames in flight, a pass issued while other
+    // renders run holds at most that many slot bytes, the frame's samples cut into equal passes
+    // of a multiple of 4; a frame that fits one pass of max_pass_bytes and is issued alone (a
+    // lone frame, the drop-in's synchronous call) still runs in one pass, in a workspace of its
+    // own. The ring's 14 workspaces then hold 32-sample passes on config 3 (6.2 GiB in all
+    // instead of 19.2, frame period alike: profiles/r05/ab/ring_pass.txt) and the lone frame
+    // keeps its single launch pair. Ring passes hold at least kRingMinSamples samples per pixel:
+    // every pass reads and writes the frame's running sums (24 B per pixel), which 4-sample
+    // passes made 5% of config 4's frame (46.6 vs 44.2 ms); below that the passes stay as they were.
+    constexpr uint64_t kRingMinSamples = 32;
+    auto ring_of = [&](uint64_t sp, uint32_t streams) -> uint64_t {
+        const uint64_t sf = std::min<uint64_t>(sp, P.spp);
+        if (streams <= 1 || !O.ring_pass_bytes) return sf;
+        const uint64_t cap = (O.ring_pass_bytes / per_sample) & ~3ull;
+        if (cap >= sf || cap < kRingMinSamples) return sf;
+        const uint64_t n = (P.spp + cap - 1) / cap;  // passes of the frame at that size
+        return std::min<uint64_t>(cap, (((P.spp + n - 1) / n) + 3u) & ~3ull);
+    };
+    // a lone frame's one pass in its own workspace (beside the ring's smaller ones)
+    auto lone_whole = [&](uint64_t sp, uint32_t streams) { return streams > 1 && sp >= P.spp && ring_of(sp, streams) < P.spp; };
+    auto dq_of = [&](uint64_t sp) -> uint64_t {
+        return may_split ? deep_queue_bytes(n_pixels, n_pixels * std::min<uint64_t>(sp, P.spp)) : 0u;
+    };
+    // the ring's workspaces (pairs when there is a ring) and the lone passes' own one (singles:
+    // a whole lone frame, or a ring pass issued alone when the ring holds pairs)
     auto footprint = [&](uint32_t streams, uint32_t wsps, uint64_t sp) -> uint64_t {
-        const uint64_t spe = std::min<uint64_t>(sp, P.spp);
-        const bool ring_pairs = pairs && streams > 1;
-        const uint64_t dq = may_split ? deep_queue_bytes(n_pixels, n_pixels * spe) : 0u;
-        uint64_t t = static_cast<uint64_t>(n_ws_of(streams, wsps)) * (ws_bytes(spe, ring_pairs) + dq);
-        if (ring_pairs) t += ws_bytes(spe, false) + dq;
-        if (sp < P.spp) t += per_sample;  // the multi-pass sums
+        const uint64_t sr = ring_of(sp, streams);
+        const bool ring_pairs = pairs && streams > 1, whole = lone_whole(sp, streams);
+        uint64_t t = static_cast<uint64_t>(n_ws_of(streams, wsps)) * (ws_bytes(sr, ring_pairs) + dq_of(sr));
+        if (whole) t += ws_bytes(sp, false) + dq_of(sp);
+        else if (ring_pairs) t += ws_bytes(sr, false) + dq_of(sr);
+        if (sr < P.spp) t += per_sample;  // the multi-pass sums
         if (wave) t += 2ull * wave_cap(sp) * 52u + 512u;
         return t;
     };
@@ -817,33 +841,34 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     }
     const bool pipe = bufs > 1;
     const uint32_t n_ws = n_ws_of(bufs, wsps);
-    const uint64_t spe = std::min<uint64_t>(spp_pass, P.spp);
-    const bool ring_pairs = pairs && pipe;
-    const uint32_t lone_ws = ring_pairs ? n_ws : kMaxWs;  // the lone passes' workspace (singles), if any
-    auto ws_size = [&](uint32_t w) { return ws_bytes(spe, ring_pairs && w != lone_ws); };
+    const uint64_t spe = std::min<uint64_t>(spp_pass, P.spp);  // a lone pass
+    const uint64_t spr = ring_of(spp_pass, bufs);                // a ring pass
+    const bool ring_pairs = pairs && pipe, whole = lone_whole(spp_pass, bufs);
+    const uint32_t lone_ws = (ring_pairs || whole) ? n_ws : kMaxWs;  // the lone passes' workspace (singles), if any
+    auto pass_of = [&](uint32_t w) { return w == lone_ws && whole ? spe : spr; };
+    auto ws_size = [&](uint32_t w) { return ws_bytes(pass_of(w), ring_pairs && w != lone_ws); };
     // under a cap, workspaces left larger (or more numerous) by earlier frames are re-cut once
     if (O.max_workspace_bytes) {
         uint64_t after = 0;
         for (uint32_t w = 0; w < kMaxWs; ++w) {
             const bool used = w < n_ws || w == lone_ws;
             after += used ? std::max<uint64_t>(sc->slots_bytes[w], ws_size(w)) : sc->slots_bytes[w];
-            after += used && may_split ? std::max<uint64_t>(sc->deep_bytes[w], deep_queue_bytes(n_pixels, n_pixels * spe))
-                                       : sc->deep_bytes[w];
+            after += used && may_split ? std::max<uint64_t>(sc->deep_bytes[w], dq_of(pass_of(w))) : sc->deep_bytes[w];
         }
-        after += spp_pass < P.spp ? std::max<uint64_t>(sc->acc_bytes, per_sample) : sc->acc_bytes;
+        after += spr < P.spp ? std::max<uint64_t>(sc->acc_bytes, per_sample) : sc->acc_bytes;
         after += wave ? std::max<uint64_t>(sc->wq_bytes, 2ull * wave_cap(spp_pass) * 52u + 512u) : sc->wq_bytes;
         if (after > O.max_workspace_bytes)
             if (int rc = free_workspaces(sc); rc) return rc;
     }
     sc->used_streams = bufs;
-    sc->used_ws = n_ws + (ring_pairs ? 1u : 0u);
-    sc->used_pass = static_cast<uint32_t>(spe);
+    sc->used_ws = n_ws + (lone_ws < kMaxWs ? 1u : 0u);
+    sc->used_pass = static_cast<uint32_t>(spr);
     sc->used_deep = 0;
-    if (spp_pass < P.spp)
+    if (spr < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
     for (uint32_t w = 0; w < n_ws; ++w)
         if (int rc = ensure((void **)&sc->slots[w], &sc->slots_bytes[w], ws_size(w)); rc) return rc;
-    if (ring_pairs)
+    if (lone_ws < kMaxWs)
         if (int rc = ensure((void **)&sc->slots[lone_ws], &sc->slots_bytes[lone_ws], ws_size(lone_ws)); rc) return rc;
     // wavefront variant: two ray queues of cap rays (52 B each) and their counters
     uint32_t wcap = 0;
@@ -874,16 +899,20 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
 
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
-    for (uint32_t s0 = 0; s0 < P.spp; s0 += static_cast<uint32_t>(spp_pass)) {
-        const uint32_t s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + spp_pass));
+    auto others_running = [&] { return pipe && sc->last_ws >= 0 && hipEventQuery(sc->ev_done[sc->last_ws]) == hipErrorNotReady; };
+    // a frame issued alone that fits one pass takes it whole (lone_whole); otherwise ring passes
+    const uint64_t first_pass = whole && !others_running() ? spe : spr;
+    for (uint32_t s0 = 0, s1 = 0; s0 < P.spp; s0 = s1) {
+        s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + (s0 == 0 ? first_pass : spr)));
         // another render still running? (then this one takes a partial grid, grid_wg_per_cu)
-        const bool in_flight = pipe && sc->last_ws >= 0 && hipEventQuery(sc->ev_done[sc->last_ws]) == hipErrorNotReady;
+        const bool in_flight = others_running();
         // every pass takes the next workspace and stream: pass p + 1's render overlaps pass
-        // p's drain and accumulation, within a frame and across frames; a pass issued alone takes
-        // the lone passes' workspace (single samples) when the ring holds pairs
+        // p's drain and accumulation, within a frame and across frames; a whole lone frame, and
+        // a pass issued alone when the ring holds pairs, take the lone passes' workspace (single
+        // samples)
         const bool pass_pairs = ring_pairs && in_flight;
         uint32_t wb = 0;
-        if (ring_pairs && !in_flight) {
+        if (lone_ws < kMaxWs && ((s1 - s0) > spr || (ring_pairs && !in_flight))) {
             wb = lone_ws;
         } else if (pipe) {
             wb = sc->next_buf % n_ws;

@@ -72,6 +72,7 @@ rt_options library_defaults()
     o.transpose_max = 16;
     o.wave_queue_rays = 1u << 25;
     o.diag = 0;
+    o.ring_pass_bytes = 384ull << 20;
     return o;
 }
 
@@ -83,6 +84,8 @@ int check_options(const rt_options &o)
     if (o.workspaces_per_stream < 1 || o.workspaces_per_stream > kMaxWs / kMaxBufs) return bad("workspaces_per_stream (1..2)");
     if (o.deep_split > 1024) return bad("deep_split (0..1024)");
     if (o.max_pass_bytes < 12 || o.max_pass_bytes > kMaxSlotsBytes) return bad("max_pass_bytes (12 B..2 GiB)");
+    if (o.ring_pass_bytes && (o.ring_pass_bytes < 12 || o.ring_pass_bytes > kMaxSlotsBytes))
+        return bad("ring_pass_bytes (0 or 12 B..2 GiB)");
     if (o.cluster_size < 4 || o.cluster_size > 64 || o.cluster_size % 4) return bad("cluster_size (4..64, multiple of 4)");
     if (o.transpose_max > 16) return bad("transpose_max (0..16)");
     if (o.wave_queue_rays < 64) return bad("wave_queue_rays (>= 64)");
@@ -130,6 +133,7 @@ int parse_options(const char *text, rt_options &o)
         else if (key == "deep_split") ok = u32(n.deep_split);
         else if (key == "max_pass_bytes") n.max_pass_bytes = v;
         else if (key == "max_workspace_bytes") n.max_workspace_bytes = v;
+        else if (key == "ring_pass_bytes") n.ring_pass_bytes = v;
         else if (key == "deep_min_items") n.deep_min_items = v;
         else if (key == "cluster_size") ok = u32(n.cluster_size);
         else if (key == "transpose_max") ok = u32(n.transpose_max);

@@ -194,10 +194,10 @@ def test_options_defaults_and_parse():
     o = rt.options()
     assert o.size == C.sizeof(abi.RtOptions)
     assert (o.render_streams, o.workspaces_per_stream, o.deep_split, o.max_pass_bytes, o.max_workspace_bytes,
-            o.deep_min_items, o.cluster_size, o.transpose_max, o.wave_queue_rays, o.diag) == \
-        (0, 2, 8, 2 << 30, 0, 1 << 25, 16, 16, 1 << 25, 0)
-    p = rt.parse_options("render_streams=3, max_workspace_bytes=0x100000000;deep_split=0 ieee_roots=1,stats=1")
-    assert (p.render_streams, p.max_workspace_bytes, p.deep_split) == (3, 1 << 32, 0)
+            o.deep_min_items, o.cluster_size, o.transpose_max, o.wave_queue_rays, o.diag, o.ring_pass_bytes) == \
+        (0, 2, 8, 2 << 30, 0, 1 << 25, 16, 16, 1 << 25, 0, 384 << 20)
+    p = rt.parse_options("render_streams=3, max_workspace_bytes=0x100000000;deep_split=0 ieee_roots=1,stats=1,ring_pass_bytes=0")
+    assert (p.render_streams, p.max_workspace_bytes, p.deep_split, p.ring_pass_bytes) == (3, 1 << 32, 0, 0)
     assert p.diag == abi.RT_DIAG["ieee_roots"] | abi.RT_DIAG["stats"]
     assert rt.parse_options("stats=0", p).diag == abi.RT_DIAG["ieee_roots"]
     assert rt.parse_options("").render_streams == 0  # empty text: unchanged
@@ -207,6 +207,7 @@ def test_options_defaults_and_parse():
     ("render_streams=9", "render_streams"), ("workspaces_per_stream=0", "workspaces_per_stream"),
     ("workspaces_per_stream=3", "workspaces_per_stream"), ("deep_split=2000", "deep_split"),
     ("max_pass_bytes=0", "max_pass_bytes"), ("max_pass_bytes=4294967296", "max_pass_bytes"),
+    ("ring_pass_bytes=11", "ring_pass_bytes"), ("ring_pass_bytes=4294967296", "ring_pass_bytes"),
     ("cluster_size=6", "cluster_size"), ("cluster_size=68", "cluster_size"), ("transpose_max=17", "transpose_max"),
     ("wave_queue_rays=10", "wave_queue_rays"), ("diag=8192", "diag"), ("shade_lds=1,shade_global=1", "diag"),
     ("bogus=1", "bogus"), ("render_streams", "key=value"), ("render_streams=-1", "render_streams"),

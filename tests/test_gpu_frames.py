@@ -599,6 +599,41 @@ def test_workspace_cap_bounds_memory_with_the_same_bits(opts):
     ds.close()
 
 
+# ---- ring passes (rt_options.ring_pass_bytes) -----------------------------------------------
+def test_ring_passes_keep_the_bits_and_shrink_the_workspaces(opts):
+    """With frames in flight, passes issued beside other renders hold at most ring_pass_bytes of
+    slots (equal passes of a multiple of 4 samples, at least 32), while a frame issued alone runs
+    whole in a workspace of its own: frames streamed without host sync keep the bits and segment
+    counts of one-pass frames, the ring's workspaces hold the ring pass, and a ring size under 32
+    samples leaves the passes as they were."""
+    torch = pytest.importorskip("torch")
+    s, m = G.scene("huge")
+    W, H, spp = 160, 90, 96
+    cam = rt.Camera.default(W, H)
+    p = rt.make_params(W, H, spp, 64, 23)
+    want, want_st = rt.render_f32((s, m), p, cam)
+    stream = torch.cuda.current_stream().cuda_stream
+    per_sample = W * H * 12
+    for ring_samples, passes in ((40, 32), (64, 48), (28, None)):
+        ds = rt.DeviceScene((s, m), options=rt.options(render_streams=3, ring_pass_bytes=per_sample * ring_samples))
+        outs, segs = [], []
+        for _ in range(5):
+            outs.append(torch.empty((H, W, 3), dtype=torch.float32, device="cuda"))
+            segs.append(torch.zeros(3, dtype=torch.int64, device="cuda"))
+            ds.render(cam, p, outs[-1].data_ptr(), stream, segs[-1].data_ptr())
+        torch.cuda.synchronize()
+        u = ds.usage()
+        ds.close()
+        for o, g in zip(outs, segs):
+            _bits_equal(o.cpu().numpy(), want, f"ring passes of {ring_samples} samples")
+            assert int(g[0]) == want_st.segments
+        if passes is None:  # under 32 samples: no ring passes
+            assert u["pass_samples"] == spp and u["workspaces"] == 6, u
+        else:  # 96 samples in 3 (2) equal passes; 6 ring workspaces + the lone one
+            assert u["pass_samples"] == passes and u["workspaces"] == 7, u
+            assert u["workspace_bytes"] >= 6 * passes * per_sample + spp * per_sample
+
+
 # ---- scenes at the LDS limit (the kernel's static LDS counts, ADVICE r3) --------------------
 def test_scene_at_the_lds_limit_renders_or_is_refused():
     """A scene whose blob fits the device's LDS per workgroup only without the render kernel's

@@ -446,6 +446,9 @@ def main():
     # wall clock ends with the device->host copy into a pinned buffer
     host_frame = torch.empty(out_frame().shape, dtype=out_frame().dtype, pin_memory=True) if rank == 0 else None
     parity = {}
+    # frames of the timed kernels this process renders (scripts/pmc_json.py divides its counters
+    # by it: a frame is one pass alone, or several ring passes beside other frames)
+    issued = [0]
 
     def measure(cam, steps, warmup, check_parity=False):
         """warmup untimed frames, then `steps` frames timed between barriers + syncs (max over
@@ -457,6 +460,7 @@ def main():
         (outside the timed region)."""
         def step(count_segments):
             ds.render(cam, params, tile.data_ptr(), stream.cuda_stream, seg.data_ptr() if count_segments else None)
+            issued[0] += 0 if count_segments else 1
             if rgb8:
                 rt.epilogue_rgb8_device(tile.data_ptr(), tile8.data_ptr(), rows * W, stream.cuda_stream)
             if not rehearse:
@@ -586,7 +590,7 @@ def main():
             "frame_latency_ms": r3(main_m["frame_latency_ms"]),
             # render streams the timed frames rotated over (frames in flight), the workspaces and
             # the samples per pass (rt_scene_usage_get after the run)
-            "frames_in_flight": usage["render_streams"], "workspaces": usage["workspaces"],
+            "frames_in_flight": usage["render_streams"], "workspaces": usage["workspaces"], "frames_issued": issued[0],
             "pass_samples": usage["pass_samples"],
             # device memory the scene held for the timed frames: HBM footprint of the product
             # (scene blobs, counters, slot workspaces, deep-path queues), and the workspaces alone

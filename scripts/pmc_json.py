@@ -45,11 +45,22 @@ def which(kernel_name):
     return next((i for i, k in enumerate(names) if matches(k, kernel_name)), None)
 
 
-# Per frame: every dispatch of the kernels in a pass summed and divided by the frames, i.e. the
-# dispatches of the first kernel (one main launch per frame for a one-pass frame such as config
-# 3; its deep launch is the second kernel's dispatch)
+# Per frame: every dispatch of the kernels in a pass summed and divided by the frames the pass's
+# bench.py run issued to them (its JSON line's frames_issued, in <pass dir>.log; a frame is one
+# pass issued alone or several ring passes beside other frames). Without that field: the first
+# kernel's dispatches (one main launch per one-pass frame).
+def pass_frames(path):
+    top = os.path.relpath(path, a.root).split(os.sep)[0]
+    try:
+        with open(os.path.join(a.root, top + ".log")) as fh:
+            line = [x for x in fh if x.startswith("{")][-1]
+        return json.loads(line).get("frames_issued") or None
+    except (OSError, IndexError, ValueError):
+        return None
+
+
 vals = defaultdict(list)
-for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(a.root, "p*", "**", "run_counter_collection.csv"), recursive=True)):
     per = defaultdict(float)
     frames = set()
     for r in csv.DictReader(open(f)):
@@ -59,12 +70,13 @@ for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_counter_collection.csv
         if i == 0:
             frames.add(r["Dispatch_Id"])
         per[r["Counter_Name"]] += float(r["Counter_Value"])
+    nf = pass_frames(f) or len(frames)
     for c, v in per.items():
-        vals[c].append(v / len(frames))
+        vals[c].append(v / nf)
 dur = []
-for f in sorted(glob.glob(os.path.join(a.root, "p*", "run_kernel_trace.csv"))):
+for f in sorted(glob.glob(os.path.join(a.root, "p*", "**", "run_kernel_trace.csv"), recursive=True)):
     rows = [r for r in csv.DictReader(open(f)) if which(r["Kernel_Name"]) is not None]
-    n = sum(1 for r in rows if which(r["Kernel_Name"]) == 0)
+    n = pass_frames(f) or sum(1 for r in rows if which(r["Kernel_Name"]) == 0)
     if n:
         dur.append(sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9 for r in rows) / n)
 m = {c: sum(v) / len(v) for c, v in vals.items()}

@@ -19,5 +19,13 @@ constexpr float kIsoR2Grow = 1.0201f;
 // a dielectric sphere's shortcut word (rt_host.cpp shortcut_words): this bit, then the geo slots
 // (+ 1, 0 = none) of its at most two neighbours in bits [0, 15) and [15, 30)
 constexpr uint32_t kShortcut = 0x80000000u;
+// clusters under one level-2 box (the walk tests a passing box's clusters in pairs). 8: config 3
+// frame period 2.548-2.562 vs 2.578-2.596 ms with 4, 6 alike with 4, 12 and 16 slower, 2 +5%
+// (profiles/r05/ab/super_clusters.txt)
+#ifndef RT_SUPER
+#define RT_SUPER 8
+#endif
+constexpr uint32_t kSuperClusters = RT_SUPER;
+static_assert(kSuperClusters % 2 == 0, "clusters are tested in pairs");
 
 } // namespace rt

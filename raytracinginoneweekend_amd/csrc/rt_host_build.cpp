@@ -410,14 +410,15 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered, uint32_t clust
     } else {
         for (uint32_t i = 0; i < n; ++i) always.push_back(i);
     }
-    // clusters: the big ones, padded to a multiple of 4 (an empty slot never passes), then the
-    // small ones; each group of 4 consecutive clusters gets a level-2 box
+    // clusters: the big ones, padded to a multiple of kSuperClusters (an empty slot never
+    // passes), then the small ones; each group of kSuperClusters consecutive clusters gets a
+    // level-2 box
     std::vector<std::vector<uint32_t>> clusters;
     if (!big.empty()) split_clusters(s, big, clusters, cluster_max);
-    while (clusters.size() % 4) clusters.emplace_back();
+    while (clusters.size() % rt::kSuperClusters) clusters.emplace_back();
     if (!small.empty()) split_clusters(s, small, clusters, cluster_max);
-    // clusters stay in the DFS order of the median-split tree: 4 consecutive clusters are a
-    // depth-2 subtree, spatially tight, and become one level-2 box
+    // clusters stay in the DFS order of the median-split tree: 8 consecutive clusters are a
+    // depth-3 subtree, spatially tight, and become one level-2 box
 
     auto pad4 = [](uint32_t x) { return (x + 3u) & ~3u; };
     std::vector<float> geo;
@@ -474,9 +475,9 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered, uint32_t clust
     b.n_geo = static_cast<uint32_t>(sidx.size());
     b.n_clusters = static_cast<uint32_t>(clusters.size());
     b.n_clusters_real = b.n_clusters;
-    // pad to a multiple of 4 clusters (grouped box tests) with boxes no ray enters:
+    // pad to a multiple of kSuperClusters clusters (grouped box tests) with boxes no ray enters:
     // negative extents make t_in > t_out whatever the ray
-    while (b.n_clusters % 4) {
+    while (b.n_clusters % rt::kSuperClusters) {
         uint32_t packed = static_cast<uint32_t>(sidx.size());  // count 0
         float pf;
         std::memcpy(&pf, &packed, 4);
@@ -495,11 +496,11 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered, uint32_t clust
     }
     b.clus_offset = static_cast<uint32_t>(b.data.size() / 4);
     b.data.insert(b.data.end(), crec.begin(), crec.end());
-    // level 2: one box over every 4 consecutive clusters (padding clusters contribute nothing)
+    // level 2: one box over every kSuperClusters consecutive clusters (padding clusters contribute nothing)
     b.supers_offset = static_cast<uint32_t>(b.data.size() / 4);
-    for (uint32_t g = 0; g < b.n_clusters; g += 4) {
+    for (uint32_t g = 0; g < b.n_clusters; g += rt::kSuperClusters) {
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (uint32_t c = g; c < std::min(g + 4, b.n_clusters_real); ++c)
+        for (uint32_t c = g; c < std::min(g + rt::kSuperClusters, b.n_clusters_real); ++c)
             for (int a = 0; a < 3; ++a) {
                 lo[a] = std::min(lo[a], boxes[6 * c + a]);
                 hi[a] = std::max(hi[a], boxes[6 * c + 3 + a]);
@@ -514,7 +515,7 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered, uint32_t clust
             kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
             b.clus_pad = std::max(b.clus_pad, kc);
         }
-        uint32_t packed = g | (4u << 16);
+        uint32_t packed = g | (rt::kSuperClusters << 16);
         float pf;
         std::memcpy(&pf, &packed, 4);
         b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});

@@ -790,7 +790,7 @@ __device__ __forceinline__ Hit closest_hit(const KP &p, const float4 *__restrict
         // Two levels under a root box, with whole-wave control (lanes predicated by `active`) so
         // that every lane can take part in a cluster's transposed member tests: the level-3 box
         // over every cluster gates the walk (a ray that misses the padded union box misses every
-        // padded box inside it), a level-2 box covers 4 consecutive clusters, and a passing
+        // padded box inside it), a level-2 box covers kSuperClusters (8) consecutive clusters, and a passing
         // level-2 box's cluster boxes are tested in pairs against the current t_best.
         const RayBox rb{ix, iy, iz, oix, oiy, oiz, aix, aiy, aiz, px, py, pz};
         const float4 *sup = clus + (p.supers_offset - p.clus_offset);
@@ -813,8 +813,8 @@ __device__ __forceinline__ Hit closest_hit(const KP &p, const float4 *__restrict
             const bool sp = bs & active;
             RT_EV(EV_SUPER_PASS);
             const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
-            wt.add_box(4u * (uint32_t)__popcll(spm));
-            for (uint32_t c = c0i; c < c0i + 4; c += 2) {
+            wt.add_box(kSuperClusters * (uint32_t)__popcll(spm));
+            for (uint32_t c = c0i; c < c0i + kSuperClusters; c += 2) {
                 const float tb_now = h.t() * 1.002f;
                 const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
                 const bool ba = box_pass(rb, a0, a1, t_lo, tb_now), bb = box_pass(rb, b0, b1, t_lo, tb_now);

@@ -388,6 +388,10 @@ void split_clusters(const rt_sphere *s, std::vector<uint32_t> ids, std::vector<s
     split_clusters(s, std::move(right), out, kClusterMax);
 }
 
+#ifndef RT_SUPER_FULL
+#define RT_SUPER_FULL 0  // A/B build switch: every level-2 box's clusters walked, empty ones too
+#endif
+constexpr bool kSuperCount = RT_SUPER_FULL != 0;
 blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered, uint32_t cluster_max)
 {
     // three classes by |r| against the median: huge (> 64x, e.g. the ground) are tested on
@@ -515,7 +519,15 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered, uint32_t clust
             kc = kPadRel * (std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + E[0] + E[1] + E[2]) + 1e-6f;
             b.clus_pad = std::max(b.clus_pad, kc);
         }
-        uint32_t packed = g | (rt::kSuperClusters << 16);
+        // the clusters the walk tests under this box: up to its last non-empty one, in pairs (the
+        // big spheres' group is padded to kSuperClusters with empty clusters no ray enters)
+        uint32_t cn = kSuperCount ? rt::kSuperClusters : 0u;
+        if (!kSuperCount) {
+            for (uint32_t c = g; c < std::min(g + rt::kSuperClusters, b.n_clusters_real); ++c)
+                if (!clusters[c].empty()) cn = c - g + 1u;
+            cn = (cn + 1u) & ~1u;
+        }
+        uint32_t packed = g | (cn << 16);
         float pf;
         std::memcpy(&pf, &packed, 4);
         b.data.insert(b.data.end(), {C[0], C[1], C[2], E[0], E[1], E[2], kc, pf});

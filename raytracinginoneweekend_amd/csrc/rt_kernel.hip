@@ -812,9 +812,10 @@ __device__ __forceinline__ Hit closest_hit(const KP &p, const float4 *__restrict
             if (!spm) continue;
             const bool sp = bs & active;
             RT_EV(EV_SUPER_PASS);
-            const uint32_t c0i = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)) & 0xffffu;
-            wt.add_box(kSuperClusters * (uint32_t)__popcll(spm));
-            for (uint32_t c = c0i; c < c0i + kSuperClusters; c += 2) {
+            // its first cluster and the count the walk tests (up to its last non-empty one)
+            const uint32_t sw = __builtin_amdgcn_readfirstlane(__float_as_uint(s1.w)), c0i = sw & 0xffffu, cn = sw >> 16;
+            wt.add_box(cn * (uint32_t)__popcll(spm));
+            for (uint32_t c = c0i; c < c0i + cn; c += 2) {
                 const float tb_now = h.t() * 1.002f;
                 const float4 a0 = clus[2 * c], a1 = clus[2 * c + 1], b0 = clus[2 * c + 2], b1 = clus[2 * c + 3];
                 const bool ba = box_pass(rb, a0, a1, t_lo, tb_now), bb = box_pass(rb, b0, b1, t_lo, tb_now);

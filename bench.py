@@ -76,6 +76,7 @@ def parse():
                     help="cull: exact cluster culling (same bits); brute: every sphere, as the reference")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip dropin_first_ms / dropin_repeat_ms")
     ap.add_argument("--cpu-rows", type=int, default=240, help="rows in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this job may use (cpu_info)")
     ap.add_argument("--rehearse-world", type=int, default=0,
@@ -278,6 +279,78 @@ def pmc_fields(path, kernel, config):
     return rec, "current build of the timed kernel"
 
 
+
+
+# Issue cost of one wave64 VALU instruction per SIMD, cycles, by PMC class, as measured on gfx950
+# with 8 waves per SIMD (scripts/ubench_int.hip, profiles/r02/ubench_int.txt): plain f32 add/mul/fma
+# and 32-bit integer ops ~2.4 (an SGPR operand, integer multiplies, bfe/add3/lshl_add take ~4.2:
+# the INT32 and F32 classes mix both, so 2.4 is their floor); 64-bit integer ~4.2; transcendental
+# (rcp, sqrt) ~8.2. The VALU count the typed counters leave over is compares, v_cndmask,
+# conversions, min/max/med3, DPP, moves and f64: counted at ~4.2 (moves issue at ~2.3: an
+# estimate, not a measurement of the mix).
+ISSUE_CYCLES = {"plain": 2.4, "int64": 4.2, "trans": 8.2, "other": 4.2}
+
+
+def issue_roofline(pmc, ms_per_step):
+    """The VALU issue roofline: sum over PMC instruction classes of count x
+    measured issue cycles, over 1024 SIMDs x the PMC run's clock x the frame period."""
+    c = pmc.get("counters", {})
+    need = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32",
+            "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_TRANS_F32")
+    if any(k not in c for k in need):
+        return {"issue_frac": None}
+    plain = c["SQ_INSTS_VALU_ADD_F32"] + c["SQ_INSTS_VALU_MUL_F32"] + c["SQ_INSTS_VALU_FMA_F32"] + c["SQ_INSTS_VALU_INT32"]
+    int64, trans = c["SQ_INSTS_VALU_INT64"], c["SQ_INSTS_VALU_TRANS_F32"]
+    other = max(0.0, c["SQ_INSTS_VALU"] - plain - int64 - trans)
+    cyc = (plain * ISSUE_CYCLES["plain"] + int64 * ISSUE_CYCLES["int64"] + trans * ISSUE_CYCLES["trans"]
+           + other * ISSUE_CYCLES["other"])
+    cap = 1024 * pmc["clock_ghz"] * 1e9 * ms_per_step * 1e-3
+    tot = c["SQ_INSTS_VALU"]
+    # the same at the nominal issue rates (a wave64 VALU instruction over 2 cycles on a SIMD-32,
+    # MI355X_MICROARCH.md; half-rate shapes 4, transcendentals 8)
+    nom = plain * 2.0 + int64 * 4.0 + trans * 8.0 + other * 4.0
+    return {"issue_frac": round(cyc / cap, 4), "issue_frac_nominal": round(nom / cap, 4),
+            "issue_cycles_per_frame": round(cyc),
+            "issue_mix": {"plain_f32_int32": round(plain / tot, 4), "int64": round(int64 / tot, 4),
+                          "trans": round(trans / tot, 4), "other_estimated": round(other / tot, 4)},
+            "issue_model": "cycles/wave-inst: plain 2.4 (floor: SGPR operands and 4.2-cycle integer shapes "
+                           "inside the class are not separable), int64 4.2, trans 8.2, the VALU count the typed "
+                           "counters leave over (compares, selects, conversions, min/max, DPP, moves) 4.2, "
+                           "an estimate; capacity = 1024 SIMDs x the PMC run's clock x ms_per_step"}
+
+
+def dropin_timing(arrays, cam, W, H, spp, depth, seed, repeats=3):
+    """The reference's entry as a caller meets it (cuda_impl, called once per frame at
+    main.cxx:114 into the caller's vector of main.cxx:112): rt_render_rgb8 into a host buffer
+    allocated once, through the synchronous C-ABI path (rt::render_impl's), timed on the host
+    from call to return: the first call (scene build, workspaces, frame buffers) and repeats
+    (the kept per-device context)."""
+    import ctypes as C
+    import numpy as np
+    import raytracinginoneweekend_amd as rt
+    from raytracinginoneweekend_amd import _abi as abi
+    s, m = arrays
+    s = np.ascontiguousarray(s, dtype=abi.SPHERE_DTYPE)
+    m = np.ascontiguousarray(m, dtype=abi.MATERIAL_DTYPE)
+    out = np.zeros((H, W, 3), dtype=np.uint8)
+    p = rt.make_params(W, H, spp, depth, seed)
+    st = abi.RtStats()
+    rt.release_cached()
+
+    def call():
+        t0 = time.perf_counter()
+        rt._lib.check(rt.lib().rt_render_rgb8(abi.ptr(s, C.POINTER(abi.RtSphere)), len(s),
+                                              abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m), C.byref(cam.c),
+                                              C.byref(p), abi.ptr(out, C.POINTER(C.c_uint8)), C.byref(st)))
+        return (time.perf_counter() - t0) * 1e3
+
+    first = call()
+    rep = sorted(call() for _ in range(repeats))
+    rt.release_cached()
+    return {"dropin_first_ms": round(first, 3), "dropin_repeat_ms": round(rep[len(rep) // 2], 3),
+            "dropin_repeat_all_ms": [round(x, 3) for x in rep], "dropin_kernel_ms": round(st.kernel_ms, 3),
+            "dropin_entry": "rt_render_rgb8 (rt::render_impl's entry): scene, render, u8 epilogue, D2H into "
+                            "the caller's buffer; host clock call to return"}
 
 
 def cpu_info():
@@ -608,7 +681,6 @@ def main():
                 "work": "executed ray-sphere tests x 20 FLOP + cluster-box tests x 19 FLOP per frame, over the "
                         "frame period (ms_per_step)",
                 "flop_per_frame": main_m["flop_per_frame"],
-                "frac_unpacked": round(main_m["achieved"] / PEAK_FP32_TFLOPS * 2, 4),
                 # brute-force equivalent (segments x spheres x 20 FLOP over the period): a speed-up
                 # figure over the reference's algorithm, NOT a fraction of any peak
                 "effective_tflops": round(main_m["effective_tflops"], 2),
@@ -632,9 +704,10 @@ def main():
             rec["roofline"]["traffic"] = pmc["hbm_bytes_per_frame"]
             rec["roofline"]["traffic_unit"] = "bytes/frame"
             rec["roofline"]["valu_insts_per_frame"] = pmc["valu_insts"]
-            # VALU pipe busy over the frame period: wave64 VALU = 2 cycles, 1024 SIMDs
+            # VALU pipe busy over the frame period: wave64 VALU = 2 cycles, 1024 SIMDs (a floor)
             rec["roofline"]["valu_busy"] = round(
                 pmc["valu_insts"] * 2.0 / (1024 * pmc["clock_ghz"] * 1e9 * main_m["ms_per_step"] * 1e-3), 4)
+            rec["roofline"].update(issue_roofline(pmc, main_m["ms_per_step"]))
             rec["roofline"]["pmc_source"] = os.path.relpath(args.pmc, REPO)
         if parity:
             rec["parity"] = parity
@@ -669,6 +742,9 @@ def main():
                     "projected_frame_wall_ms": r3(main_m["frame_wall_ms"] + xgmi_ms),
                     "note": "rehearsed on one GPU, not measured: rank 0's rows alone, the gather's device copies "
                             "and the full-frame D2H copy stood in; xGMI transfer time estimated"}
+        if world == 1 and not rehearse and not compat and args.variant == "exact" and args.traversal == "cull" \
+                and not args.no_dropin:
+            rec.update(dropin_timing(arrays, cam, W, H, spp, depth, args.seed))
         if world == 1 and not args.no_cpu_baseline and not rehearse:
             rec["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], args.camera, args.seed, args.cpu_rows,
                                                args.cpu_threads)

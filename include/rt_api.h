@@ -184,8 +184,15 @@ enum rt_diag {
                                           without the lane's own bound (the pre-fd383c3 form),
                                           for the bounds check to report (rt_scene_debug_counters) */
     RT_DIAG_NO_PAIRS = 1u << 11,        /* one sample per item and slot, under a cap too        */
-    RT_DIAG_PAIRS = 1u << 12            /* sample pairs for passes in flight without a cap
+    RT_DIAG_PAIRS = 1u << 12,           /* sample pairs for passes in flight without a cap
                                           (otherwise taken only under max_workspace_bytes)    */
+    RT_DIAG_IN_FLIGHT = 1u << 13,       /* every pass planned as if issued beside other renders
+                                          (partial grid, ring pass, pairs if asked): tests of
+                                          that plan that must not depend on timing             */
+    RT_DIAG_NATURAL_ORDER = 1u << 14,   /* items dealt in the pixels' natural tile order (no
+                                          tile classes, no sky path)           */
+    RT_DIAG_NO_SKY = 1u << 15           /* tile classes order the dealing, but samples of tiles
+                                          proven to reach the sky trace their segment          */
 };
 int rt_options_default(rt_options *out);
 /* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,
@@ -221,6 +228,13 @@ int rt_scene_huge(uint32_t seed, rt_sphere *spheres, uint32_t sphere_cap, uint32
                   rt_material *materials, uint32_t material_cap, uint32_t *n_materials);
 
 /* ---- synchronous host-buffer renders (the cuda_impl replacement) ------------------- */
+/* These keep one device context per device between calls (the scene on the device, its
+ * workspaces, the frame buffers), keyed by the scene's records and the process-default
+ * options: a repeated call with the same scene renders without rebuilding anything, as the
+ * reference's main() calls its entry once per frame (src/main.cxx:114). Another scene or
+ * other default options rebuild it. Calls are serialised within the process.
+ * rt_release_cached frees every such context (its device memory and streams).           */
+int rt_release_cached(void);
 /* Linear (pre-gamma) averaged RGB, f32. rgb_out: see rt_params output layout.          */
 int rt_render_f32(const rt_sphere *spheres, uint32_t n_spheres,
                   const rt_material *materials, uint32_t n_materials,
@@ -295,6 +309,12 @@ typedef struct rt_scene_usage {
     uint32_t deep_launch;      /* the last render's last deep-path launch: waves per workgroup
                                   (4: beside other renders; 8: a lone pass, shading records in
                                   LDS) | 16 when it dealt its chunks statically; 0 = none      */
+    uint32_t pair_passes;      /* passes of the last render that stored sample pairs          */
+    uint32_t split_passes;     /* passes of the last render with a deep-path launch           */
+    uint32_t lead_tiles;       /* the last pass: 64-pixel tiles dealt first (a primary can meet
+                                  a dielectric sphere), 0 = natural order      */
+    uint32_t sky_tiles;        /* the last pass: tiles whose primaries are proven to reach the
+                                  sky (dealt last, no closest-hit test)                        */
 } rt_scene_usage;
 int rt_scene_usage_get(const rt_scene *scene, rt_scene_usage *out);
 /* Spans (ms, HIP events) of the render kernels of the most recent calls of

@@ -71,7 +71,8 @@ class RtSceneUsage(C.Structure):
     _fields_ = [
         ("device_bytes", C.c_uint64), ("workspace_bytes", C.c_uint64), ("render_streams", C.c_uint32),
         ("workspaces", C.c_uint32), ("pass_samples", C.c_uint32), ("static_lds_bytes", C.c_uint32),
-        ("max_lds_bytes", C.c_uint32), ("deep_launch", C.c_uint32),
+        ("max_lds_bytes", C.c_uint32), ("deep_launch", C.c_uint32), ("pair_passes", C.c_uint32),
+        ("split_passes", C.c_uint32), ("lead_tiles", C.c_uint32), ("sky_tiles", C.c_uint32),
     ]
 
 
@@ -79,6 +80,7 @@ RT_DIAG = {
     "ieee_roots": 1 << 0, "no_shortcut": 1 << 1, "no_neighbours": 1 << 2, "no_root_box": 1 << 3,
     "shade_lds": 1 << 4, "shade_global": 1 << 5, "stats": 1 << 6, "stats_deep_only": 1 << 7, "verbose": 1 << 8,
     "standin_transport": 1 << 9, "unbounded_nb": 1 << 10, "no_pairs": 1 << 11, "pairs": 1 << 12,
+    "in_flight": 1 << 13, "natural_order": 1 << 14, "no_sky": 1 << 15,
 }
 
 
@@ -95,7 +97,7 @@ MATERIAL_DTYPE = np.dtype([("kind", "<u4"), ("albedo", "<f4", (3,)), ("param", "
 assert SPHERE_DTYPE.itemsize == C.sizeof(RtSphere) == 20
 assert MATERIAL_DTYPE.itemsize == C.sizeof(RtMaterial) == 20
 assert C.sizeof(RtParams) == 40
-assert C.sizeof(RtOptions) == 64 and C.sizeof(RtSceneUsage) == 40
+assert C.sizeof(RtOptions) == 64 and C.sizeof(RtSceneUsage) == 56
 
 
 def ptr(arr, ctype=C.c_void_p):

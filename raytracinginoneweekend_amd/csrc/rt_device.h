@@ -106,7 +106,7 @@ struct KParams {
     const float4 *blob;
     uint32_t blob_units;     // 16-byte units
     uint32_t n_geo, n_always, n_clusters, clus_offset;
-    uint32_t n_supers, supers_offset;  // level 2: groups of 4 consecutive clusters, 2 float4 each
+    uint32_t n_supers, supers_offset;  // level 2: groups of kSuperClusters (8) consecutive clusters, 2 float4 each
     uint32_t use_root;       // level 3: one box over all clusters at supers_offset + 2 n_supers
     uint32_t iso;            // isolated-sphere shortcut of the walk (rt_kernel.hip hint_candidate)
     uint32_t transpose_max;  // clusters requested by at most this many lanes (<= 16) are tested transposed

@@ -34,7 +34,7 @@ hipError_t launch_render(int variant, int cull, const KParams &p, uint32_t grid,
 #define RT_LONE_DEEP_TMAX 4u  // the lone deep launch's transposition threshold (below)
 #endif
 hipError_t deep_occupancy(int variant, int wpb, size_t lds, int *blocks_per_cu, size_t *static_lds);
-hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds);
+hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds, bool pairs = false);
 hipError_t static_lds_render(int variant, int cull, size_t *bytes, bool pairs = false);
 hipError_t launch_accumulate(const KAccum &k, hipStream_t stream);
 hipError_t launch_compat(const KCompat &k, uint32_t grid, hipStream_t stream);
@@ -177,6 +177,7 @@ struct rt_scene {
     bool tail_valid = false;
     int cu_count = 0;
     int occ[4][2][2];  // [variant][culled][shade records in LDS] blocks per CU, -1 = unknown
+    int occ_pairs[4][2];  // the culled kernel's sample-pair instantiation, [variant][shade records in LDS]
     // [variant] blocks per CU of the 8-wave deep kernel with the whole blob in LDS, -1 = unknown,
     // 0 = it does not fit or holds no more waves than 4-wave groups (the lone deep launch)
     int occ_deep_wide[4] = {-1, -1, -1, -1};
@@ -188,7 +189,8 @@ struct rt_scene {
     size_t static_lds[2] = {0, 0};
     size_t static_lds_pairs = 0;  // the culled kernel's sample-pair instantiation (its parked colours)
     // the last render's cut (rt_scene_usage_get)
-    uint32_t used_streams = 0, used_ws = 0, used_pass = 0, used_deep = 0;
+    uint32_t used_streams = 0, used_ws = 0, used_pass = 0, used_deep = 0, used_pairs = 0, used_split = 0;
+    uint32_t used_lead = 0, used_sky = 0;  // the last pass's tile classes
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
     static constexpr uint32_t kRing = 256;
     std::vector<hipEvent_t> ev_begin, ev_end;
@@ -341,9 +343,13 @@ uint32_t render_streams_of(const rt_options &o)
 }
 
 
-int ensure(void **ptr, size_t *have, size_t want)
+// *fresh (optional): set when the buffer was (re)allocated, whatever address it got back (the
+// allocator may return the freed one; ADVICE r5: callers key their resets on this, not on the address)
+int ensure(void **ptr, size_t *have, size_t want, bool *fresh = nullptr)
 {
+    if (fresh) *fresh = false;
     if (*have >= want && *ptr) return RT_OK;
+    if (fresh) *fresh = true;
     if (*ptr) {
         RT_HIP(hipDeviceSynchronize());
         RT_HIP(hipFree(*ptr));
@@ -468,6 +474,7 @@ int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_ma
     rt_scene *sc = new rt_scene();
     sc->opt = opt;
     for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
+    for (auto &r : sc->occ_pairs) r[0] = r[1] = -1;
     sc->in_fast_range = true;
     for (uint32_t i = 0; i < n_spheres; ++i) {
         for (float v : {spheres[i].center[0], spheres[i].center[1], spheres[i].center[2], spheres[i].radius})
@@ -756,6 +763,17 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // brute force and the scalar-cache variant store single samples).
     const bool pairs_ok = !wave && cull_mode == 7 && variant != rt::V_EXACT_SCALAR && !(O.diag & RT_DIAG_NO_PAIRS) &&
                           lds + sc->static_lds_pairs <= sc->max_lds;
+    // the pair instantiation's own occupancy (its parked colours add static LDS): the
+    // grid of a paired pass is sized by it
+    int occ_pr = occ;
+    if (pairs_ok) {
+        int &o = sc->occ_pairs[variant][k.shade_lds ? 1 : 0];
+        if (o < 0) {
+            RT_HIP(rt::occupancy_render(variant, cull_mode, &o, lds, true));
+            o = std::max(o, 1);
+        }
+        occ_pr = o;
+    }
     bool pairs = pairs_ok && (O.diag & RT_DIAG_PAIRS);
     const uint32_t full_blocks_end = P.spp & ~3u;  // samples [0, full_blocks_end) form blocks of 4
     auto slot_rows = [&](uint64_t a, uint64_t b, bool pr) -> uint64_t {  // samples [a, b), a a multiple of 4
@@ -864,6 +882,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     sc->used_ws = n_ws + (lone_ws < kMaxWs ? 1u : 0u);
     sc->used_pass = static_cast<uint32_t>(spr);
     sc->used_deep = 0;
+    sc->used_pairs = sc->used_split = sc->used_lead = sc->used_sky = 0;
     if (spr < P.spp)
         if (int rc = ensure((void **)&sc->acc, &sc->acc_bytes, per_sample); rc) return rc;
     for (uint32_t w = 0; w < n_ws; ++w)
@@ -901,11 +920,11 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     ++sc->calls;
     auto others_running = [&] { return pipe && sc->last_ws >= 0 && hipEventQuery(sc->ev_done[sc->last_ws]) == hipErrorNotReady; };
     // a frame issued alone that fits one pass takes it whole (lone_whole); otherwise ring passes
-    const uint64_t first_pass = whole && !others_running() ? spe : spr;
+    const uint64_t first_pass = whole && !others_running() && !(O.diag & RT_DIAG_IN_FLIGHT) ? spe : spr;
     for (uint32_t s0 = 0, s1 = 0; s0 < P.spp; s0 = s1) {
         s1 = static_cast<uint32_t>(std::min<uint64_t>(P.spp, s0 + (s0 == 0 ? first_pass : spr)));
         // another render still running? (then this one takes a partial grid, grid_wg_per_cu)
-        const bool in_flight = others_running();
+        const bool in_flight = others_running() || (pipe && (O.diag & RT_DIAG_IN_FLIGHT));
         // every pass takes the next workspace and stream: pass p + 1's render overlaps pass
         // p's drain and accumulation, within a frame and across frames; a whole lone frame, and
         // a pass issued alone when the ring holds pairs, take the lone passes' workspace (single
@@ -933,12 +952,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.sample_begin = s0;
         k.sample_end = s1;
         k.n_pair_items = static_cast<uint32_t>(((s1 - s0) - slot_rows(s0, s1, pass_pairs)) * n_pixels);
+        if (k.n_pair_items) ++sc->used_pairs;
         fill_frame_consts(k);
         // items: the pass's pair items and its single tail samples (one slot each)
         const uint64_t n_samples = n_pixels * (s1 - s0);
         k.n_items = static_cast<uint32_t>(n_pixels * slot_rows(s0, s1, pass_pairs));
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(occ, in_flight, bufs, n_samples)) * sc->cu_count, (k.n_items + 255u) / 256u)));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(pass_pairs ? occ_pr : occ, in_flight, bufs, n_samples)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u, in_flight);
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
@@ -949,9 +969,10 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         if (may_split && (n_samples >= O.deep_min_items || in_flight)) {
             const uint32_t rcap = deep_region_cap(n_samples), cap = 8u * rcap;
             const size_t px_bytes = deep_px_bytes(n_pixels);
-            void *had = sc->deep[wb];
-            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], deep_queue_bytes(n_pixels, n_samples)); rc) return rc;
-            if (sc->deep[wb] != had) {  // new memory: no flag set, no pair arrival counted
+            bool fresh = false;
+            if (int rc = ensure(&sc->deep[wb], &sc->deep_bytes[wb], deep_queue_bytes(n_pixels, n_samples), &fresh); rc)
+                return rc;
+            if (fresh) {  // new memory: no flag set, no pair arrival counted
                 sc->deep_clean[wb] = 0;
                 RT_HIP(hipMemsetAsync(sc->deep[wb], 0, sc->deep_bytes[wb], xst));
             } else if (sc->deep_meet_at[wb] != px_bytes + static_cast<size_t>(cap) * 56u) {
@@ -1013,6 +1034,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 RT_HIP(hipEventRecord(sc->ev_main[wb], xst));
             }
             if (k.deep_depth) {  // the deep launch: the queued paths, same grid, same stream
+                ++sc->used_split;
                 rt::KParams kd = k;
                 kd.deep_mode = k.deep_depth;
                 kd.deep_depth = 0;
@@ -1228,6 +1250,10 @@ int rt_scene_usage_get(const rt_scene *sc, rt_scene_usage *out)
     u.workspaces = sc->used_ws;
     u.pass_samples = sc->used_pass;
     u.deep_launch = sc->used_deep;
+    u.pair_passes = sc->used_pairs;
+    u.split_passes = sc->used_split;
+    u.lead_tiles = sc->used_lead;
+    u.sky_tiles = sc->used_sky;
     u.static_lds_bytes = static_cast<uint32_t>(sc->static_lds[1]);
     u.max_lds_bytes = static_cast<uint32_t>(sc->max_lds);
     *out = u;
@@ -1296,52 +1322,112 @@ int rt_epilogue_rgb8_device(const float *d_rgb, uint8_t *d_out, uint64_t n_pixel
 
 namespace {
 
+// The synchronous renders' per-device context, kept between calls: the reference's entry point
+// (cuda_impl, src/CUDA/cuda_impl.cu:384-453) is called once per frame with the same scene, and
+// building the scene (clusters, shortcut words, streams, events), its workspaces and the frame
+// buffers on every call cost more than the frame itself. The context is keyed by the scene's
+// records and the options its scene would be created with (rt_get_default_options at the call):
+// another scene or other options rebuild it. rt_release_cached frees it.
+struct SyncContext {
+    std::vector<unsigned char> key;
+    rt_scene *sc = nullptr;
+    float *d_rgb = nullptr;
+    size_t rgb_bytes = 0;
+    uint8_t *d_u8 = nullptr;
+    size_t u8_bytes = 0;
+    uint64_t *d_seg = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+std::mutex g_sync_mu;  // one synchronous render at a time per process (the reference's entry is not re-entrant)
+std::map<int, SyncContext> g_sync;
+
+void sync_release(int dev, SyncContext &c)
+{
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(dev);
+    if (c.sc) rt_scene_destroy(c.sc);
+    for (void *p : {(void *)c.d_rgb, (void *)c.d_u8, (void *)c.d_seg})
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : {c.e0, c.e1})
+        if (e) (void)hipEventDestroy(e);
+    c = SyncContext{};
+    (void)hipSetDevice(prev);
+}
+
 // Synchronous host-buffer render on the current device (the cuda_impl replacement).
 int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
                 const rt_camera *camera, const rt_params *params, float *rgb_out, uint8_t *u8_out, rt_stats *stats)
 {
     if (!camera || (!rgb_out && !u8_out)) return fail(RT_ERR_INVALID, "render: null argument");
     if (int rc = check_params(params); rc != RT_OK) return rc;
+    if ((n_spheres && !spheres) || !materials || !n_materials) return fail(RT_ERR_INVALID, "render: null scene");
     const auto t0 = std::chrono::steady_clock::now();
     int dev = 0;
     RT_HIP(hipGetDevice(&dev));
-    rt_scene *sc = nullptr;
-    if (int rc = rt_scene_create(spheres, n_spheres, materials, n_materials, dev, &sc); rc) return rc;
+    std::lock_guard<std::mutex> lock(g_sync_mu);
+    SyncContext &cx = g_sync[dev];
+    {
+        rt_options opt;
+        if (int rc = rt_get_default_options(&opt); rc) return rc;
+        std::vector<unsigned char> key(sizeof(rt_sphere) * n_spheres + sizeof(rt_material) * n_materials + sizeof(opt));
+        unsigned char *k = key.data();
+        if (n_spheres) std::memcpy(k, spheres, sizeof(rt_sphere) * n_spheres);
+        k += sizeof(rt_sphere) * n_spheres;
+        std::memcpy(k, materials, sizeof(rt_material) * n_materials);
+        k += sizeof(rt_material) * n_materials;
+        std::memcpy(k, &opt, sizeof(opt));
+        if (!cx.sc || key != cx.key) {
+            sync_release(dev, cx);
+            if (int rc = rt_scene_create(spheres, n_spheres, materials, n_materials, dev, &cx.sc); rc) return rc;
+            cx.key.swap(key);
+        }
+    }
+    rt_scene *sc = cx.sc;
     const rt_params &P = *params;
     const uint64_t rows = (P.flags & RT_FLAG_FULL_FRAME) ? P.height : rows_of(P);
     const uint64_t n_values = rows * P.width * 3u;
-    float *d_rgb = nullptr;
-    uint8_t *d_u8 = nullptr;
-    uint64_t *d_seg = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
     int rc = RT_OK;
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
         return rc == RT_OK;
     };
-    if (chk(hipMalloc((void **)&d_rgb, n_values * 4), "hipMalloc") && u8_out) chk(hipMalloc((void **)&d_u8, n_values), "hipMalloc");
-    if (rc == RT_OK) chk(hipMalloc((void **)&d_seg, 24), "hipMalloc");
-    if (rc == RT_OK && (P.flags & RT_FLAG_FULL_FRAME)) chk(hipMemset(d_rgb, 0, n_values * 4), "hipMemset");
-    if (rc == RT_OK) chk(hipMemset(d_seg, 0, 24), "hipMemset");
-    if (rc == RT_OK) chk(hipEventCreate(&e0), "hipEventCreate");
-    if (rc == RT_OK) chk(hipEventCreate(&e1), "hipEventCreate");
+    auto grow_buf = [&](void **p, size_t *have, size_t want) {
+        if (*have >= want && *p) return;
+        if (*p) chk(hipFree(*p), "hipFree");
+        *p = nullptr;
+        *have = 0;
+        if (chk(hipMalloc(p, std::max<size_t>(want, 256)), "hipMalloc")) *have = want;
+    };
+    grow_buf((void **)&cx.d_rgb, &cx.rgb_bytes, n_values * 4);
+    if (u8_out) grow_buf((void **)&cx.d_u8, &cx.u8_bytes, n_values);
+    if (rc == RT_OK && !cx.d_seg) chk(hipMalloc((void **)&cx.d_seg, 24), "hipMalloc");
+    if (rc == RT_OK && !cx.e0) chk(hipEventCreate(&cx.e0), "hipEventCreate");
+    if (rc == RT_OK && !cx.e1) chk(hipEventCreate(&cx.e1), "hipEventCreate");
+    float *d_rgb = cx.d_rgb;
+    uint8_t *d_u8 = cx.d_u8;
+    uint64_t *d_seg = cx.d_seg;
+    hipEvent_t e0 = cx.e0, e1 = cx.e1;
+    if (rc == RT_OK && (P.flags & RT_FLAG_FULL_FRAME)) chk(hipMemsetAsync(d_rgb, 0, n_values * 4, nullptr), "hipMemset");
+    if (rc == RT_OK) chk(hipMemsetAsync(d_seg, 0, 24, nullptr), "hipMemset");
     if (rc == RT_OK) chk(hipEventRecord(e0, nullptr), "hipEventRecord");
     if (rc == RT_OK) rc = rt_render_device(sc, camera, params, d_rgb, nullptr, d_seg);
     if (rc == RT_OK) chk(hipEventRecord(e1, nullptr), "hipEventRecord");
     if (rc == RT_OK && u8_out) rc = rt_epilogue_rgb8_device(d_rgb, d_u8, n_values / 3, nullptr);
-    if (rc == RT_OK) chk(hipDeviceSynchronize(), "render");
     uint64_t segs[3] = {0, 0, 0};
     float ms = 0.f;
+    // the copies on the null stream follow the render; the last one returns when all is done
     if (rc == RT_OK && rgb_out) chk(hipMemcpy(rgb_out, d_rgb, n_values * 4, hipMemcpyDeviceToHost), "hipMemcpy");
     if (rc == RT_OK && u8_out) chk(hipMemcpy(u8_out, d_u8, n_values, hipMemcpyDeviceToHost), "hipMemcpy");
     if (rc == RT_OK) chk(hipMemcpy(segs, d_seg, 24, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == RT_OK) chk(hipDeviceSynchronize(), "render");
     if (rc == RT_OK) chk(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-    if (d_rgb) (void)hipFree(d_rgb);
-    if (d_u8) (void)hipFree(d_u8);
-    if (d_seg) (void)hipFree(d_seg);
-    rt_scene_destroy(sc);
+    if (rc != RT_OK) {
+        // a failed call leaves no state behind: the next one starts from a new context
+        const std::string msg = g_error;
+        sync_release(dev, cx);
+        g_error = msg;
+    }
     if (rc == RT_OK && stats) {
         stats->primaries = static_cast<uint64_t>(P.width) * rows_of(P) * P.spp;
         stats->segments = segs[0];
@@ -1356,6 +1442,14 @@ int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material 
 } // namespace
 
 extern "C" {
+
+int rt_release_cached(void)
+{
+    std::lock_guard<std::mutex> lock(g_sync_mu);
+    for (auto &kv : g_sync) sync_release(kv.first, kv.second);
+    g_sync.clear();
+    return RT_OK;
+}
 
 int rt_render_f32(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
                   const rt_camera *camera, const rt_params *params, float *rgb_out, rt_stats *stats)

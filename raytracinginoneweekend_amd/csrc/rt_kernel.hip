@@ -75,6 +75,8 @@ enum DbgEvent : uint32_t {
     EV_ISO_LANES,   // lanes that skipped the cluster walk (isolated hint sphere), summed over iterations
     EV_WALK_SKIPPED,  // wave iterations with segments whose cluster walk no lane needed
     EV_WALK1, EV_WALK2, EV_WALK4, EV_WALK8,  // wave iterations whose walk 1, 2, 3-4, 5-8 lanes need
+    EV_PAIR_SUM,   // (lanes) pair sums stored by the main launch (both samples ended there)
+    EV_BOTH_MEET,  // (lanes) pair sums formed in the deep launch by the second of two queued samples
     EV_COUNT
 };
 static_assert(EV_COUNT <= kDbgEvents, "event counters");
@@ -1206,6 +1208,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     const f3 cp = mk(__uint_as_float(atomicOr(fw + partner, 0u)), __uint_as_float(atomicOr(fw + cap + partner, 0u)),
                                      __uint_as_float(atomicOr(fw + 2u * cap + partner, 0u)));
                     col = role == kRoleBothFirst ? col + cp : cp + col;  // RN(c_2j + c_2j+1)
+                    if (STATS) ++dbg.ev[EV_BOTH_MEET];
                     atomicExch(P.deep.meet + first, 0u);               // zero again for the next pass
                 }
             } else {
@@ -1220,7 +1223,10 @@ __device__ __forceinline__ void render_body(const KParams &p)
                         return true;
                     }
                     // the first's colour, unless it went to the deep queue (which then adds this one)
-                    if (!(it & kItFirstDeep)) col = mk(park(0, sl), park(1, sl), park(2, sl)) + col;  // RN(c_2j + c_2j+1)
+                    if (!(it & kItFirstDeep)) {
+                        col = mk(park(0, sl), park(1, sl), park(2, sl)) + col;  // RN(c_2j + c_2j+1)
+                        if (STATS) ++dbg.ev[EV_PAIR_SUM];
+                    }
                 }
                 dst = P.slots + (size_t)checked<STATS>(slot, P.n_items, BC_SLOT, p.dbg) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
             }
@@ -1328,8 +1334,8 @@ __device__ __forceinline__ void render_body(const KParams &p)
             }
         }
         stamp(1);
-        // no live lane: the item space is exhausted, or every lane's metal path was absorbed
-        // above (the refill then continues with the wave's chunk)
+        // no live lane: the wave's refill found the item space exhausted (a metal path absorbed
+        // above stays alive until finish() stores its colour at the end of this iteration)
         if (ballot(alive) == 0) {
             if (exhausted) break;
             continue;
@@ -2193,9 +2199,9 @@ hipError_t deep_occupancy(int variant, int wpb, size_t lds, int *blocks_per_cu, 
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64 * wpb, lds);
 }
 
-hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds)
+hipError_t occupancy_render(int variant, int cull, int *blocks_per_cu, size_t lds, bool pairs)
 {
-    const void *fn = render_ptr(variant, cull, false);
+    const void *fn = render_ptr(variant, cull, false, pairs);
     if (!fn) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 256, lds);
 }

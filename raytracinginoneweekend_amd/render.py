@@ -115,6 +115,11 @@ def render_rgb8(scene, params, camera=None):
     return out, st
 
 
+def release_cached():
+    """rt_release_cached: free the device context the synchronous renders keep between calls."""
+    check(lib().rt_release_cached())
+
+
 def render_multi_f32(scene, params, ngpu=0, camera=None):
     """Row-interleaved render over `ngpu` devices of this process, gathered with RCCL."""
     s, m = _scene_arrays(scene)
@@ -244,7 +249,7 @@ class DeviceScene:
     EVENTS = ["iter", "refill_trip", "fresh", "reject_trip", "lens_done", "scatter_done", "root_gate_pass", "super",
               "super_pass", "cluster_req", "transposed", "t_round", "t_far", "per_lane_members", "sky", "hit",
               "lambert", "unit_dir", "dielectric", "store", "metal_absorb", "live_lanes", "dry_iter", "dry_lanes",
-              "iso_lanes", "walk_skipped", "walk_1", "walk_2", "walk_3_4", "walk_5_8"]
+              "iso_lanes", "walk_skipped", "walk_1", "walk_2", "walk_3_4", "walk_5_8", "pair_sums", "both_deep_meets"]
 
     def debug_events(self, reset=True):
         """Block-execution counts of the instrumented kernel (options stats=True), see rt_scene_debug_events."""
@@ -253,9 +258,11 @@ class DeviceScene:
         return dict(zip(self.EVENTS, list(buf)))
 
     def debug_timeline(self, max_waves=65536):
-        """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry (the deep launch:
-        iterations in which the wave walked the clusters), start, cycles) of the
-        last instrumented launch (options stats=True; dry = when the wave found every queue empty;
+        """Per-wave (dry, exit, iterations, cu_id, refills, iterations_after_dry, start, cycles) of
+        the last instrumented launch (options stats=True). For a deep launch two fields hold walk
+        counts instead: dry = (walks with a walking lane that has no hint sphere) << 32 | walks,
+        iterations_after_dry = iterations in which the wave walked the clusters. Otherwise dry =
+        when the wave found every queue empty;
         times in ticks of the 100 MHz clock; cycles = shader-clock cycles in the loop, so
         cycles / (exit - start) x 100 MHz is the clock the wave ran at), see rt_scene_debug_timeline."""
         buf = (C.c_uint64 * (4 * max_waves))()

@@ -378,35 +378,46 @@ def test_deep_split_overflow_feedback(opts):
 
 
 
-@pytest.mark.parametrize("streams", [1, 0])
-def test_sample_pairs_through_the_deep_queue(streams, opts):
+def test_sample_pairs_through_the_deep_queue(opts):
     """Sample pairs whose samples leave for the deep queue: with the split at 1
     segment most continuing paths go there, so pairs end with one sample in each launch (the
     first's or the second's colour left in the pair slot) or with both queued (they meet through
     device-scope atomics, the second to end sums). Frames of different sizes and sample counts
     (pairs and single tail samples, several passes) follow each other on one scene, so every
     workspace's deep queue is laid out anew between passes (its pair-arrival words must start at
-    zero); one workspace (render_streams = 1) or the default rotation. Each frame equals the
-    oracle bit for bit, as does the unpaired render (the default without a workspace cap)."""
+    zero). Every pass is planned as one issued beside other renders (diag in_flight: ring passes
+    on the render streams, pairs taken every pass, not only when a render happens to be running;
+    ADVICE r5), and the test checks that they were: rt_scene_usage.pair_passes for every frame,
+    and, in the instrumented kernel, pair sums formed in the main launch and both-deep meets in
+    the deep launch. Each frame equals the oracle bit for bit, as does the unpaired render."""
     torch = pytest.importorskip("torch")
     s, m = _glass_scene_frames()
     # one pass budget for the scene (8 samples of the largest frame): the frames below are cut
     # into passes of different sizes, single tail samples included
-    opts.set(deep_min_items=0, deep_split=1, render_streams=streams, max_pass_bytes=80 * 44 * 12 * 8, pairs=True)
+    opts.set(deep_min_items=0, deep_split=1, render_streams=0, max_pass_bytes=80 * 44 * 12 * 8, pairs=True,
+             in_flight=True)
     cases = [(64, 40, 10), (48, 30, 23), (80, 44, 16), (40, 24, 7), (64, 40, 10), (80, 44, 26)]
-    ds = rt.DeviceScene((s, m))
     stream = torch.cuda.current_stream().cuda_stream
-    outs = []
-    for W, H, spp in cases:
-        o = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-        ds.render(rt.Camera.default(W, H), rt.make_params(W, H, spp, 64, 31), o.data_ptr(), stream)
-        outs.append(o)
-    torch.cuda.synchronize()
-    ds.close()
-    for (W, H, spp), o in zip(cases, outs):
-        want, _ = O.render_f32(s, m, O.camera_default(W, H), rt.make_params(W, H, spp, 64, 31))
-        _bits_equal(o.cpu().numpy(), want, f"{W}x{H} spp {spp}")
-    opts.set(pairs=False)
+    for stats in (False, True):
+        opts.set(stats=stats)
+        ds = rt.DeviceScene((s, m))
+        outs = []
+        for W, H, spp in cases:
+            o = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+            ds.render(rt.Camera.default(W, H), rt.make_params(W, H, spp, 64, 31), o.data_ptr(), stream)
+            u = ds.usage()
+            assert u["pair_passes"] >= 1 and u["split_passes"] >= 1, (W, H, spp, u)
+            outs.append(o)
+        torch.cuda.synchronize()
+        if stats:
+            ev = ds.debug_events()
+            assert ev["pair_sums"] > 0 and ev["both_deep_meets"] > 0, ev
+            ds.debug_counters()  # raises on a bounds-check violation
+        ds.close()
+        for (W, H, spp), o in zip(cases, outs):
+            want, _ = O.render_f32(s, m, O.camera_default(W, H), rt.make_params(W, H, spp, 64, 31))
+            _bits_equal(o.cpu().numpy(), want, f"{W}x{H} spp {spp} stats {stats}")
+    opts.set(pairs=False, in_flight=False, stats=False)
     W, H, spp = cases[1]
     img, _ = rt.render_f32((s, m), rt.make_params(W, H, spp, 64, 31))
     want, _ = O.render_f32(s, m, O.camera_default(W, H), rt.make_params(W, H, spp, 64, 31))
@@ -457,7 +468,12 @@ def test_lone_deep_launch_static_dealing_runs(opts):
     ds.render(cam, p, outs[0].data_ptr(), stream, segs[0].data_ptr())
     torch.cuda.synchronize()
     lone = ds.usage()["deep_launch"]
-    for o, g in zip(outs[1:], segs[1:]):  # back to back: the later ones start while others run
+    ds.close()
+    # the in-flight plan, forced (diag in_flight) so that it does not depend on whether a render
+    # is still running when the next call arrives
+    opts.set(in_flight=True)
+    ds = rt.DeviceScene((s, m))
+    for o, g in zip(outs[1:], segs[1:]):
         ds.render(cam, p, o.data_ptr(), stream, g.data_ptr())
     flight = ds.usage()["deep_launch"]
     torch.cuda.synchronize()

@@ -227,6 +227,16 @@ int rt_camera_cuda(uint32_t width, uint32_t height, rt_camera *out);
 int rt_scene_huge(uint32_t seed, rt_sphere *spheres, uint32_t sphere_cap, uint32_t *n_spheres,
                   rt_material *materials, uint32_t material_cap, uint32_t *n_materials);
 
+/* The dealing order of the pass that camera + params describe on this scene:
+ * its 64-pixel blocks (8x8 tiles, then row-major blocks of leftover rows) as dealt, perm[i] =
+ * the natural block of dealing position i; n_lead blocks first (a primary ray can meet a
+ * cluster's box), n_sky blocks last (every primary ray proven to meet no sphere: those samples
+ * skip the closest-hit test). n_blocks = 0: the pass keeps the natural order (its pixel count is
+ * not a multiple of 64). cap = 0 queries the counts. Host-only (no device needed).            */
+int rt_tile_order(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials,
+                  uint32_t n_materials, const rt_camera *camera, const rt_params *params,
+                  uint32_t *perm, uint32_t cap, uint32_t *n_blocks, uint32_t *n_lead, uint32_t *n_sky);
+
 /* ---- synchronous host-buffer renders (the cuda_impl replacement) ------------------- */
 /* These keep one device context per device between calls (the scene on the device, its
  * workspaces, the frame buffers), keyed by the scene's records and the process-default

@@ -8,7 +8,7 @@ from .camera import CORRECTED, REFERENCE, Camera  # noqa: F401
 from .render import (DeviceScene, MultiContext, default_options, default_options_set,  # noqa: F401
                      epilogue_rgb8_device, make_params, options, parse_options, render_cuda_impl, render_f32,
                      release_cached, render_multi_f32, render_multi_rgb8, render_rgb8, save_ppm,
-                     set_default_options)
+                     set_default_options, tile_order)
 from .scene import (Dielectric, Lambert, Metal, RaytracerData, Sphere, cuda_scene_arrays, huge_scene,  # noqa: F401
                     huge_scene_arrays, simple_scene, simple_scene_arrays)
 

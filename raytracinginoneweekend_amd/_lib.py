@@ -42,6 +42,9 @@ def _declare(L):
         "rt_camera_cuda": (C.c_int, [C.c_uint32, C.c_uint32, P(abi.RtCamera)]),
         "rt_render_cuda_impl": (C.c_int, [C.c_uint32, C.c_uint32, P(C.c_uint8)]),
         "rt_release_cached": (C.c_int, []),
+        "rt_tile_order": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32, P(abi.RtCamera),
+                                    P(abi.RtParams), P(C.c_uint32), C.c_uint32, P(C.c_uint32), P(C.c_uint32),
+                                    P(C.c_uint32)]),
         "rt_render_f32": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32,
                                     P(abi.RtCamera), P(abi.RtParams), P(C.c_float), P(abi.RtStats)]),
         "rt_render_rgb8": (C.c_int, [P(abi.RtSphere), C.c_uint32, P(abi.RtMaterial), C.c_uint32,

@@ -191,6 +191,19 @@ struct rt_scene {
     // the last render's cut (rt_scene_usage_get)
     uint32_t used_streams = 0, used_ws = 0, used_pass = 0, used_deep = 0, used_pairs = 0, used_split = 0;
     uint32_t used_lead = 0, used_sky = 0;  // the last pass's tile classes
+    // the culled scene's geometry for the tile classes of a pass, and the
+    // dealing orders computed from it, per camera and rows (a pure function of those and the
+    // scene, kept for the kOrders most recently used), each with its block permutation on the device
+    rthost::scene_geom geom;
+    bool has_geom = false;
+    struct Order {
+        std::vector<unsigned char> key;
+        rthost::tile_order t;
+        uint32_t *d_perm = nullptr;
+        uint64_t used = 0;
+    };
+    static constexpr size_t kOrders = 8;
+    std::vector<Order> orders;
     // ring of (start, end) events bracketing the render kernels of each rt_render_device call
     static constexpr uint32_t kRing = 256;
     std::vector<hipEvent_t> ev_begin, ev_end;
@@ -395,6 +408,8 @@ int rt_scene_destroy(rt_scene *sc)
     for (void *p : sc->deep)
         if (p) (void)hipFree(p);
     if (sc->deep_over) (void)hipHostFree(sc->deep_over);
+    for (auto &o : sc->orders)
+        if (o.d_perm) (void)hipFree(o.d_perm);
     (void)hipSetDevice(prev);
     delete sc;
     return RT_OK;
@@ -473,6 +488,10 @@ int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_ma
     }
     rt_scene *sc = new rt_scene();
     sc->opt = opt;
+    if (blobs[1].n_clusters) {
+        sc->geom = scene_geometry(spheres, blobs[1]);
+        sc->has_geom = true;
+    }
     for (auto &r : sc->occ) for (auto &x : r) x[0] = x[1] = -1;
     for (auto &r : sc->occ_pairs) r[0] = r[1] = -1;
     sc->in_fast_range = true;
@@ -554,6 +573,46 @@ int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_ma
 }
 
 namespace {
+// The dealing order of a pass over these rows with this camera (rt_scene::orders; computed on a
+// miss: classify_tiles on the host, the permutation uploaded once).
+int pass_order(rt_scene *sc, const rt_camera &cam, const rt::KParams &k, const rt_scene::Order **out)
+{
+    *out = nullptr;
+    std::vector<unsigned char> key(sizeof(rt_camera) + 7 * sizeof(uint32_t));
+    const uint32_t g[7] = {k.W, k.H, k.row_offset, k.row_stride, k.num_rows, k.tile_lw, 0u};
+    std::memcpy(key.data(), &cam, sizeof(rt_camera));
+    std::memcpy(key.data() + sizeof(rt_camera), g, sizeof(g));
+    static uint64_t tick = 0;
+    for (auto &o : sc->orders)
+        if (o.key == key) {
+            o.used = ++tick;
+            *out = &o;
+            return RT_OK;
+        }
+    rt_scene::Order e;
+    e.key.swap(key);
+    e.t = classify_tiles(cam, k.W, k.H, k.row_offset, k.row_stride, k.num_rows, k.tile_lw, sc->geom);
+    if (!e.t.perm.empty()) {
+        RT_HIP(hipMalloc((void **)&e.d_perm, e.t.perm.size() * sizeof(uint32_t)));
+        const hipError_t ce = hipMemcpy(e.d_perm, e.t.perm.data(), e.t.perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (ce != hipSuccess) {
+            (void)hipFree(e.d_perm);
+            return fail(RT_ERR_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(ce));
+        }
+    }
+    if (sc->orders.size() >= rt_scene::kOrders) {
+        auto lru = std::min_element(sc->orders.begin(), sc->orders.end(),
+                                    [](const rt_scene::Order &a, const rt_scene::Order &b) { return a.used < b.used; });
+        RT_HIP(hipDeviceSynchronize());  // renders in flight may still read its permutation
+        if (lru->d_perm) RT_HIP(hipFree(lru->d_perm));
+        sc->orders.erase(lru);
+    }
+    e.used = ++tick;
+    sc->orders.push_back(std::move(e));
+    *out = &sc->orders.back();
+    return RT_OK;
+}
+
 int free_workspaces(rt_scene *sc)
 {
     RT_HIP(hipDeviceSynchronize());
@@ -763,6 +822,9 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     // brute force and the scalar-cache variant store single samples).
     const bool pairs_ok = !wave && cull_mode == 7 && variant != rt::V_EXACT_SCALAR && !(O.diag & RT_DIAG_NO_PAIRS) &&
                           lds + sc->static_lds_pairs <= sc->max_lds;
+    // passes dealt by tile classes: the culled LDS kernels with a scene geometry to classify
+    const bool order_ok = sc->has_geom && cull_mode == 7 && !wave && variant != rt::V_EXACT_SCALAR &&
+                          !(O.diag & RT_DIAG_NATURAL_ORDER);
     // the pair instantiation's own occupancy (its parked colours add static LDS): the
     // grid of a paired pass is sized by it
     int occ_pr = occ;
@@ -953,6 +1015,12 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.sample_end = s1;
         k.n_pair_items = static_cast<uint32_t>(((s1 - s0) - slot_rows(s0, s1, pass_pairs)) * n_pixels);
         if (k.n_pair_items) ++sc->used_pairs;
+        // dealing order: lead tiles first and proven sky tiles last in every
+        // queue's share (single-sample passes of the culled LDS kernels), else the natural order
+        const rt_scene::Order *ord = nullptr;
+        if (order_ok && !k.n_pair_items)
+            if (int rc = pass_order(sc, *camera, k, &ord); rc) return rc;
+        const bool ordered = ord && ord->d_perm;
         fill_frame_consts(k);
         // items: the pass's pair items and its single tail samples (one slot each)
         const uint64_t n_samples = n_pixels * (s1 - s0);
@@ -961,12 +1029,38 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(pass_pairs ? occ_pr : occ, in_flight, bufs, n_samples)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u, in_flight);
+        k.block_perm = nullptr;
+        k.n_groups = 1;
+        k.sky_group = 0;
+        k.grp_blocks[0] = k.n_blocks;
+        k.grp_items0 = k.n_items;
+        if (ordered) {
+            const rthost::tile_order &t = ord->t;
+            const uint64_t S = s1 - s0;
+            const uint64_t nbl[3] = {t.n_lead, t.perm.size() - t.n_lead - t.n_sky, t.n_sky};
+            k.block_perm = ord->d_perm;
+            k.n_groups = 3;
+            k.sky_group = (O.diag & RT_DIAG_NO_SKY) ? 0u : 1u;
+            k.grp_pix[0] = 0;
+            for (int g = 0; g < 3; ++g) {
+                k.grp_pix[g + 1] = k.grp_pix[g] + static_cast<uint32_t>(64u * nbl[g]);
+                k.div_grp[g] = make_udiv(static_cast<uint32_t>(std::max<uint64_t>(64u * nbl[g], 1u)));
+                k.grp_blocks[g] = static_cast<uint32_t>(nbl[g] * S);  // nbl[g] blocks per sample
+            }
+            k.grp_items0 = 64u * k.grp_blocks[0];
+            sc->used_lead = t.n_lead;
+            sc->used_sky = k.sky_group ? t.n_sky : 0u;
+        } else {
+            sc->used_lead = sc->used_sky = 0;
+        }
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
         k.deep_depth = 0;
         k.deep_mode = 0;
         bool two_part = false;
         uint32_t stats_waves = 0;  // the instrumented build: waves of the launch the counters cover
-        if (may_split && (n_samples >= O.deep_min_items || in_flight)) {
+        // a lone pass dealt by tile classes is not split: its trapped paths start in its first
+        // items and end inside the bulk of the launch
+        if (may_split && (n_samples >= O.deep_min_items || in_flight) && (in_flight || !ordered)) {
             const uint32_t rcap = deep_region_cap(n_samples), cap = 8u * rcap;
             const size_t px_bytes = deep_px_bytes(n_pixels);
             bool fresh = false;
@@ -1126,6 +1220,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         if (pipe && d_segments) a.seg_from = seg_b, a.seg_to = reinterpret_cast<unsigned long long *>(d_segments);
         a.queue_reset = k.queue_ctr;
         a.queue_words = 8 * rt::kQueueStride;
+        a.block_perm = k.block_perm;
         if (k.deep_depth) {
             a.deep_over = sc->deep_over_dev + wb;
             a.deep_key = deep_key;

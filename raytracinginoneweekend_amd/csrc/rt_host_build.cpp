@@ -631,6 +631,169 @@ std::vector<uint32_t> shortcut_words(const rt_sphere *s, uint32_t n, const rt_ma
     return word;
 }
 
+// ---- tile classes --------------------------------------------------------
+scene_geom scene_geometry(const rt_sphere *s, const blob_t &b)
+{
+    scene_geom g;
+    for (uint32_t i : b.always) g.always.push_back(s[i]);
+    g.clus_pad = b.clus_pad;
+    // cluster records {C, E, pad, start | count << 16} at clus_offset, 8 floats each
+    for (uint32_t c = 0; c < b.n_clusters; ++c) {
+        const float *r = b.data.data() + 4u * b.clus_offset + 8u * c;
+        uint32_t packed;
+        std::memcpy(&packed, r + 7, 4);
+        if ((packed >> 16) == 0u || !(r[3] >= 0.f)) continue;  // empty or padding cluster
+        g.boxes.insert(g.boxes.end(), r, r + 6);
+    }
+    if (b.n_clusters) {
+        // the level-3 box follows the n_supers level-2 boxes
+        const float *r = b.data.data() + 4u * b.supers_offset + 8u * b.n_supers;
+        if (r[3] >= 0.f) {
+            std::copy(r, r + 6, g.root);
+            g.has_root = true;
+        }
+    }
+    return g;
+}
+
+namespace {
+// closed intervals in double: every operation's result contains every value its operands can take
+struct iv {
+    double lo, hi;
+};
+iv operator+(iv a, iv b) { return {a.lo + b.lo, a.hi + b.hi}; }
+iv operator-(iv a, iv b) { return {a.lo - b.hi, a.hi - b.lo}; }
+iv operator-(iv a, double c) { return {a.lo - c, a.hi - c}; }
+iv operator*(iv a, iv b)
+{
+    const double p[4] = {a.lo * b.lo, a.lo * b.hi, a.hi * b.lo, a.hi * b.hi};
+    return {std::min(std::min(p[0], p[1]), std::min(p[2], p[3])), std::max(std::max(p[0], p[1]), std::max(p[2], p[3]))};
+}
+iv operator*(double c, iv a) { return c >= 0 ? iv{c * a.lo, c * a.hi} : iv{c * a.hi, c * a.lo}; }
+iv sq(iv a)
+{
+    if (a.lo >= 0) return {a.lo * a.lo, a.hi * a.hi};
+    if (a.hi <= 0) return {a.hi * a.hi, a.lo * a.lo};
+    return {0.0, std::max(a.lo * a.lo, a.hi * a.hi)};
+}
+iv grow(iv a, double e) { return {a.lo - e, a.hi + e}; }
+double mag(iv a) { return std::max(std::fabs(a.lo), std::fabs(a.hi)); }
+
+// Every ray o + t d (t >= 0) with o in the box o[], d in the box d[] misses the box [lo, hi]:
+// the t for which a coordinate of some ray of the beam can lie in the slab form one interval
+// per axis (o_lo + t d_lo <= hi and o_hi + t d_hi >= lo), which contains each single ray's
+// slab interval; if the three have no common t >= 0, no ray of the beam meets the box.
+bool beam_misses(const iv o[3], const iv d[3], const double lo[3], const double hi[3])
+{
+    double t0 = 0.0, t1 = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+        const double a = hi[k] - o[k].lo;  // t d_lo <= a
+        if (d[k].lo > 0) t1 = std::min(t1, a / d[k].lo);
+        else if (d[k].lo < 0) t0 = std::max(t0, a / d[k].lo);
+        else if (a < 0) return true;
+        const double b = lo[k] - o[k].hi;  // t d_hi >= b
+        if (d[k].hi > 0) t0 = std::max(t0, b / d[k].hi);
+        else if (d[k].hi < 0) t1 = std::min(t1, b / d[k].hi);
+        else if (b > 0) return true;
+    }
+    // empty with a relative margin far above the double divisions' rounding
+    return t1 < 0 || t0 > t1 * (1 + 1e-9) + 1e-12;
+}
+
+// No ray of the beam gets a candidate from sphere S in the kernel's binary32 test
+// (raytracer.hxx:52-92 as rt_kernel.hip test_block8 evaluates it), proven in exact arithmetic
+// with margins of 1e-5 of the terms' magnitudes, where the binary32 evaluation errs by < 2^-21:
+// either the discriminant b^2 - a c is negative for every ray, or every ray starts outside S
+// (c > 0) moving away from it (b > 0) with b 2^-22 < kMIN a / 2, so that both roots are negative
+// and the rounded far root stays below kMIN (the kernel's own shortcut for the ground, whose
+// condition the float values then meet too).
+bool sphere_missed(const iv o[3], const iv d[3], const rt_sphere &S)
+{
+    const iv oc[3] = {o[0] - static_cast<double>(S.center[0]), o[1] - static_cast<double>(S.center[1]),
+                      o[2] - static_cast<double>(S.center[2])};
+    const double r2 = static_cast<double>(S.radius) * S.radius;
+    const iv a = sq(d[0]) + sq(d[1]) + sq(d[2]);
+    const iv b = oc[0] * d[0] + oc[1] * d[1] + oc[2] * d[2];
+    const iv c = (sq(oc[0]) + sq(oc[1]) + sq(oc[2])) - r2;
+    const double bm = mag(oc[0]) * mag(d[0]) + mag(oc[1]) * mag(d[1]) + mag(oc[2]) * mag(d[2]);
+    const double cm = mag(oc[0]) * mag(oc[0]) + mag(oc[1]) * mag(oc[1]) + mag(oc[2]) * mag(oc[2]) + r2;
+    const iv disc = sq(b) - a * c;
+    if (disc.hi < -1e-5 * (bm * bm + a.hi * cm)) return true;
+    return b.lo > 1e-5 * bm && c.lo > 1e-5 * cm && b.hi * 0x1p-22 < 0.5 * 0.008 * a.lo;
+}
+} // namespace
+
+tile_order classify_tiles(const rt_camera &cam, uint32_t W, uint32_t H, uint32_t row_offset, uint32_t row_stride,
+                          uint32_t num_rows, uint32_t tile_lw, const scene_geom &g, bool sky_only)
+{
+    tile_order out;
+    const uint64_t n_pixels = static_cast<uint64_t>(W) * num_rows;
+    if (!W || !H || n_pixels == 0 || n_pixels % 64u || tile_lw > 6u) return out;  // natural order
+    const uint32_t n_blocks = static_cast<uint32_t>(n_pixels / 64u);
+    const uint32_t tw = 1u << tile_lw, th = 64u >> tile_lw;
+    const bool tiled = W % tw == 0u;
+    const uint32_t tiles_x = tiled ? W / tw : 1u, tiled_rows = tiled ? (num_rows / th) * th : 0u;
+    const uint32_t n_tiles = tiled ? tiles_x * (tiled_rows / th) : 0u;
+    const uint32_t st = row_stride ? row_stride : 1u;
+    std::vector<uint8_t> cls(n_blocks, 1);  // 0 lead, 1 other, 2 sky; untiled blocks stay 1
+    const double lens = std::fabs(static_cast<double>(cam.lens_radius));
+    for (uint32_t t = 0; t < n_tiles; ++t) {
+        const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+        const double x0 = static_cast<double>(tx) * tw, x1 = x0 + tw;  // x in [x0, x1), jitter < 1
+        const double y0 = row_offset + static_cast<double>(ty) * th * st, y1 = y0 + static_cast<double>(th - 1) * st + 1;
+        // uu = x/W + U/W, vv = y/H + U/H in binary32 (a few ulps around the exact values)
+        const iv uu = grow({x0 / W, x1 / W}, 1e-6 * (x1 / W) + 1e-12);
+        const iv vv = grow({y0 / H, y1 / H}, 1e-6 * (y1 / H) + 1e-12);
+        const iv omv = iv{1.0, 1.0} - vv;
+        // lens offset {uu rd.x, vv rd.y, 0}, |rd_k| <= lens (camera.hxx:52-54)
+        const double ox = lens * mag(uu), oy = lens * mag(vv);
+        const iv off[3] = {{-ox, ox}, {-oy, oy}, {0.0, 0.0}};
+        iv o[3], d[3];
+        for (int k = 0; k < 3; ++k) {
+            const double org = cam.origin[k], llc = cam.lower_left_corner[k], hor = cam.horizontal[k], ver = cam.vertical[k];
+            o[k] = grow(iv{org, org} + off[k], 1e-6 * (std::fabs(org) + mag(off[k])) + 1e-30);
+            // camera.hxx:56: llc + hor u + ver (1 - v) - offset (- origin in the corrected mode)
+            iv dk = ((iv{llc, llc} + hor * uu) + ver * omv) - off[k];
+            double m = std::fabs(llc) + std::fabs(hor) * mag(uu) + std::fabs(ver) * mag(omv) + mag(off[k]);
+            if (cam.mode == RT_CAMERA_CORRECTED) {
+                dk = dk - org;
+                m += std::fabs(org);
+            }
+            d[k] = grow(dk, 1e-5 * m + 1e-30);
+        }
+        const double o1 = mag(o[0]) + mag(o[1]) + mag(o[2]);
+        // twice the kernel's per-ray pad (rt_kernel.hip closest_hit: 1e-3 |o|_1 + clus_pad)
+        const double pad = 2.0 * (1e-3 * o1 + g.clus_pad) + 1e-6;
+        auto misses_box = [&](const float *r) {
+            double lo[3], hi[3];
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = static_cast<double>(r[k]) - r[3 + k] - pad;
+                hi[k] = static_cast<double>(r[k]) + r[3 + k] + pad;
+            }
+            return beam_misses(o, d, lo, hi);
+        };
+        bool sky = !g.has_root || misses_box(g.root);
+        for (size_t i = 0; sky && i < g.always.size(); ++i) sky = sphere_missed(o, d, g.always[i]);
+        if (sky) {
+            cls[t] = 2;
+            continue;
+        }
+        if (sky_only) continue;
+        for (size_t c = 0; c + 6 <= g.boxes.size(); c += 6)
+            if (!misses_box(g.boxes.data() + c)) {
+                cls[t] = 0;
+                break;
+            }
+    }
+    out.perm.reserve(n_blocks);
+    for (uint8_t want = 0; want < 3; ++want)
+        for (uint32_t b = 0; b < n_blocks; ++b)
+            if (cls[b] == want) out.perm.push_back(b);
+    out.n_lead = static_cast<uint32_t>(std::count(cls.begin(), cls.end(), 0));
+    out.n_sky = static_cast<uint32_t>(std::count(cls.begin(), cls.end(), 2));
+    return out;
+}
+
 rt::UDiv make_udiv(uint32_t d)
 {
     rt::UDiv r{0, 0, 0};
@@ -698,6 +861,33 @@ int rt_scene_huge(uint32_t seed, rt_sphere *spheres, uint32_t sphere_cap, uint32
     scene_builder b;
     b.huge(seed);
     return b.emit(spheres, sphere_cap, n_spheres, materials, material_cap, n_materials);
+}
+
+// The dealing order a render of this scene gives the pass described by camera + params
+// (DESIGN.md §4.7): the culled blob the scene would get (default options' cluster size), then
+// classify_tiles over the pass's 8x8 tiles.
+int rt_tile_order(const rt_sphere *spheres, uint32_t n_spheres, const rt_material *materials, uint32_t n_materials,
+                  const rt_camera *camera, const rt_params *params, uint32_t *perm, uint32_t cap, uint32_t *n_blocks,
+                  uint32_t *n_lead, uint32_t *n_sky)
+{
+    if ((n_spheres && !spheres) || !materials || !camera || !params || !n_blocks || !n_lead || !n_sky || (cap && !perm))
+        return fail(RT_ERR_INVALID, "rt_tile_order: null argument");
+    (void)n_materials;
+    rt_options opt;
+    if (int rc = default_options(opt); rc) return rc;
+    const blob_t b = build_blob(spheres, n_spheres, true, opt.cluster_size);
+    const scene_geom g = scene_geometry(spheres, b);
+    const uint32_t st = params->row_stride ? params->row_stride : 1u;
+    const uint32_t rows = params->num_rows ? params->num_rows
+                          : params->row_offset >= params->height ? 0u
+                                                                 : (params->height - params->row_offset + st - 1u) / st;
+    const tile_order t = classify_tiles(*camera, params->width, params->height, params->row_offset, st, rows, 3u, g);
+    *n_blocks = static_cast<uint32_t>(t.perm.size());
+    *n_lead = t.n_lead;
+    *n_sky = t.n_sky;
+    if (t.perm.size() > cap) return cap ? fail(RT_ERR_CAPACITY, "rt_tile_order: perm buffer too small") : RT_OK;
+    std::copy(t.perm.begin(), t.perm.end(), perm);
+    return RT_OK;
 }
 
 // app::save_to_file, src/main.cxx:87-101: "P6\n<width> <height>\n255\n", then the texels.

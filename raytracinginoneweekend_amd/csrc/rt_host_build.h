@@ -40,6 +40,31 @@ blob_t build_blob(const rt_sphere *s, uint32_t n, bool clustered, uint32_t clust
 std::vector<uint32_t> shortcut_words(const rt_sphere *s, uint32_t n, const rt_material *m, const blob_t &b,
                                      bool nb_off);
 
+// ---- tile classes of a pass ---------------------------------------------
+// What the classifier needs of a culled scene: the always-tested spheres, the box of every
+// non-empty cluster and the box over all of them (centre C, half-extent E), the kernel's pad.
+struct scene_geom {
+    std::vector<rt_sphere> always;
+    std::vector<float> boxes;  // per non-empty cluster: C[3], E[3]
+    float root[6] = {0.f, 0.f, 0.f, -1.f, -1.f, -1.f};
+    bool has_root = false;
+    float clus_pad = 0.f;
+};
+scene_geom scene_geometry(const rt_sphere *s, const blob_t &b);
+// The 64-pixel blocks of a pass's pixel enumeration (tiles of 2^tile_lw x 64/2^tile_lw over
+// tiled_rows, then row-major blocks of the remaining rows) in dealing order: `lead` blocks first
+// (a primary ray of the tile can meet a cluster's padded box: the tiles whose paths can enter a
+// glass ball on their first or second segment), then the others, then `sky` blocks, whose every
+// primary ray is PROVEN to meet no sphere (interval arithmetic over the tile's rays, with
+// margins far above every float error of the kernel's tests). perm[i] = the natural block of
+// dealing block i. Empty perm: the pass keeps its natural order (pixels not in whole blocks).
+struct tile_order {
+    std::vector<uint32_t> perm;
+    uint32_t n_lead = 0, n_sky = 0;
+};
+tile_order classify_tiles(const rt_camera &cam, uint32_t W, uint32_t H, uint32_t row_offset, uint32_t row_stride,
+                          uint32_t num_rows, uint32_t tile_lw, const scene_geom &g, bool sky_only = false);
+
 rt::UDiv make_udiv(uint32_t d);
 bool exact_by_reciprocal(float b);
 

@@ -236,9 +236,12 @@ __device__ __forceinline__ uint32_t udiv(uint32_t n, const UD &u)
     return (t + ((n - t) >> u.s1)) >> u.s2;
 }
 
+// pixel (x, packed row rr) of enumeration position i; perm: the pass's block permutation
+// (KParams::block_perm) or null
 template <class FC>
-__device__ __forceinline__ void pixel_of(const FC &fc, uint32_t i, uint32_t &x, uint32_t &rr)
+__device__ __forceinline__ void pixel_of(const FC &fc, uint32_t i, uint32_t &x, uint32_t &rr, const uint32_t *perm)
 {
+    if (perm) i = (perm[i >> 6] << 6) | (i & 63u);
     const uint32_t W = fc.W, tiled_rows = fc.tiled_rows, tiles_x = fc.tiles_x;
     const uint32_t tiled_px = tiled_rows * W;
     if (i < tiled_px) {
@@ -943,6 +946,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
     // same SIMD would take ~7x as long
     if (DEEP && p.deep_prio) __builtin_amdgcn_s_setprio(3);
     // wave-uniform cursor over the item space (the deep launch: over the queued paths)
+    // (the main launch: q / 8 is the item group the wave deals from, KParams::n_groups)
     uint32_t q = blockIdx.x & 7u, q_tried = 0;
     // static dealing (KParams::deep_static): this wave's next chunk of the deep queue, in the
     // order of the regions' chunks; the grid's waves take chunks w, w + waves, w + 2 waves, ...
@@ -1076,17 +1080,20 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     cnext = __builtin_amdgcn_readfirstlane(q * P.deep.rcap + 64u * c);
                     cend = __builtin_amdgcn_readfirstlane(q * P.deep.rcap + min(64u * c + 64u, nq));
                 } else {
-                if (lane == 0) c = atomicAdd(P.queue_ctr + q * kQueueStride, 1u);
+                const uint32_t grp = q >> 3, qq = q & 7u;
+                if (lane == 0) c = atomicAdd(P.queue_ctr + qq * kQueueStride + grp, 1u);
                 c = __builtin_amdgcn_readfirstlane(c);
-                // guided: queue q owns blocks [qb0, qb1) of 64 items; ticket c takes blocks
+                // guided: queue q owns blocks [qb0, qb1) of 64 items of the group; ticket c takes blocks
                 // [S(c), S(c+1)), S(t) = min(B, floor(B (1 - beta^t)) + 2t): chunks shrink
                 // geometrically from ~B / (K waves per queue) to 2 blocks, so a queue is
                 // served by few atomics and its last chunks are small. S is the same
                 // function for every wave, so consecutive tickets tile the range; the 2t
                 // term keeps it increasing even if exp2 or the float product is off by an
                 // ulp (one block at most).
-                const uint32_t qb0 = (uint32_t)(((uint64_t)P.n_blocks * q) >> 3);
-                const uint32_t B = (uint32_t)(((uint64_t)P.n_blocks * (q + 1u)) >> 3) - qb0;
+                // the group's item blocks, an eighth per queue
+                const uint32_t GB = grp == 0u ? P.grp_blocks[0] : grp == 1u ? P.grp_blocks[1] : P.grp_blocks[2];
+                const uint32_t qb0 = (uint32_t)(((uint64_t)GB * qq) >> 3);
+                const uint32_t B = (uint32_t)(((uint64_t)GB * (qq + 1u)) >> 3) - qb0;
                 auto S = [&](uint32_t t) -> uint32_t {
                     const float x = t ? exp2f((float)t * P.guided_l2b) : 1.f;
                     const uint64_t g = (uint64_t)floorf((float)B * (1.f - x)) + 2ull * t;
@@ -1094,12 +1101,16 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 };
                 const uint32_t s0 = __builtin_amdgcn_readfirstlane(S(c));
                 if (s0 >= B) {
-                    q = (q + 1u) & 7u;
-                    if (++q_tried == 8u) exhausted = true;
+                    q = (q & ~7u) | ((q + 1u) & 7u);
+                    if (++q_tried == 8u) {  // every queue's share of the group is dealt: the next group
+                        q_tried = 0;
+                        q += 8u;
+                        if (q >= 8u * P.n_groups) exhausted = true;
+                    }
                     continue;
                 }
                 cnext = 64u * (qb0 + s0);
-                cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), P.n_items));
+                cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), grp == 0u ? P.grp_items0 : 64u * GB));
                 }
             }
         deal:
@@ -1146,6 +1157,20 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     HID(sl) = hid;
                 } else {
                     it = I;  // a pair item (the pass's full blocks) or a single tail sample; its slot
+                    if (!PAIRS && P.n_groups > 1u) {
+                        // dealt by tile classes: I indexes group grp's items,
+                        // sample-major over its positions [p0, p0 + ng); the slot is [sample][position]
+                        const uint32_t grp = q >> 3;
+                        const uint32_t p0 = grp == 0u ? 0u : grp == 1u ? P.grp_pix[1] : P.grp_pix[2];
+                        const uint32_t ng = (grp == 0u ? P.grp_pix[1] : grp == 1u ? P.grp_pix[2] : P.grp_pix[3]) - p0;
+                        const uint32_t dm = grp == 0u ? P.div_grp[0].m : grp == 1u ? P.div_grp[1].m : P.div_grp[2].m;
+                        const uint32_t d1 = grp == 0u ? P.div_grp[0].s1 : grp == 1u ? P.div_grp[1].s1 : P.div_grp[2].s1;
+                        const uint32_t d2 = grp == 0u ? P.div_grp[0].s2 : grp == 1u ? P.div_grp[1].s2 : P.div_grp[2].s2;
+                        const uint32_t t = __umulhi(I, dm);
+                        const uint32_t sg = (t + ((I - t) >> d1)) >> d2;  // udiv(I, ng)
+                        it = sg * (P.n_pixels - ng) + I + p0;
+                        if (grp == 2u && P.sky_group) it |= kItSky;
+                    }
                     alive = fresh = true;
                 }
             }
@@ -1241,7 +1266,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
         if (fresh) {
             RT_EV(EV_FRESH);
             uint32_t px, rr, ls;
-            pixel_of(*fc, item_pixel(ls), px, rr);
+            pixel_of(*fc, item_pixel(ls), px, rr, P.block_perm);
             const uint32_t py = fc->row_offset + rr * fc->row_stride;
             const uint32_t s = fc->sample_begin + ls;
             // key = (y W + x) spp + s (y W + x < 2^32: the host bounds W H)
@@ -1282,6 +1307,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
         // 64 lanes), and every stream still sees the same draws in the same order.
         bool defer = false;
         bool absorbed = false;  // a metal scatter absorbed: colour 0, finished at the iteration's end
+
         const bool lens = !DEEP && (fresh || pend_lens);
         if (lens || pend) {
             const uint64_t inc = lens ? (((uint64_t)fc->inc_cam_hi << 32) | fc->inc_cam_lo) : inc_data;
@@ -1426,6 +1452,12 @@ __device__ __forceinline__ void render_body(const KParams &p)
 
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && !defer && depth < P.max_depth;  // depth check: main.cxx:74
+        // the segments that test spheres: all but the primary rays of the tiles proven to send
+        // every primary ray to the sky (kItSky), whose segment meets no sphere:
+        // they skip the closest-hit test and take the sky colour directly (a wave of them alone
+        // runs no test at all; beside other lanes, they neither walk nor find a candidate in the
+        // always-tested spheres, by the same proof)
+        auto sky_ray = [&]() { return !DEEP && !PAIRS && depth == 0u && (it & kItSky) != 0u; };
         // |d|^2 (raytracer.hxx:56) and its refined reciprocal for this segment's roots; the sky
         // below reuses both (unit_direction's length is sqrt of the same sum)
         const float a = d.x * d.x + d.y * d.y + d.z * d.z;
@@ -1440,7 +1472,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
             if (ballot(seg && hid != ~0u))
                 key0 = hint_candidate<FAST, STATS>(seg && hid != ~0u, PN(sl), hid, NB(sl), geo, sidx, o, d, rd, P.iso,
                                                    skip, P.n_geo, P.diag_unbounded_nb, p.dbg);
-            const bool walk = seg && !skip;
+            const bool walk = seg && !skip && !sky_ray();
             const uint64_t wm = ballot(walk);
             if (STATS && first_active_lane()) {
                 dbg.ev[EV_ISO_LANES] += (uint32_t)__popcll(segm & ~wm);
@@ -1456,16 +1488,16 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 if (lane == 0 && wm) ++dbg_walks;  // iterations in which the wave walked
                 if (lane == 0 && nh) ++dbg_walks_nohint;
             }
-            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);
+            // (the lanes that skip the walk through the shortcut still test the always-tested spheres)
+            if (DEEP || (wm | ballot(skip))) h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
             h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr, no_hit());
         }
         stamp(2);
-        {
-            const uint32_t ns = lanes(seg);  // segments of this iteration (main.cxx:74 passed)
-            wt.add_seg(ns);
-            wt.add_sph((uint64_t)ns * P.n_always);
+        if (COUNT) {
+            wt.add_seg(lanes(seg));  // segments of this iteration (main.cxx:74 passed)
+            wt.add_sph((uint64_t)lanes(seg && !sky_ray()) * P.n_always);  // the always-tested spheres, executed
         }
 
         // ---- shading: the hit of every live lane -----------------------------------------
@@ -1881,17 +1913,18 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
         return;
     }
     const f3 col = acc / (float)k.spp;  // main.cxx:207
-    // output position
+    // output position (the slots' enumeration is the pass's permuted one)
     uint32_t x, rr;
     {
+        const uint32_t ni = k.block_perm ? (k.block_perm[i >> 6] << 6) | (i & 63u) : i;
         const uint32_t tiled_px = k.tiled_rows * k.W;
-        if (i < tiled_px) {
-            uint32_t t = i >> 6, w = i & 63u;
+        if (ni < tiled_px) {
+            uint32_t t = ni >> 6, w = ni & 63u;
             uint32_t ty = t / k.tiles_x, tx = t - ty * k.tiles_x;
             x = (tx << k.tile_lw) + (w & ((1u << k.tile_lw) - 1u));
             rr = (ty << (6u - k.tile_lw)) + (w >> k.tile_lw);
         } else {
-            uint32_t jj = i - tiled_px;
+            uint32_t jj = ni - tiled_px;
             rr = jj / k.W;
             x = jj - rr * k.W;
             rr += k.tiled_rows;
@@ -1936,7 +1969,7 @@ __global__ __launch_bounds__(256) void wave_gen_kernel(const KWave w)
     const uint32_t ls = udiv(I, fc.div_n_pixels);
     const uint32_t pix = I - ls * fc.n_pixels;
     uint32_t px, rr;
-    pixel_of(fc, pix, px, rr);
+    pixel_of(fc, pix, px, rr, nullptr);  // (the wavefront variant deals in natural order)
     const uint32_t py = fc.row_offset + rr * fc.row_stride;
     const uint32_t sm = fc.sample_begin + ls;
     const uint64_t inc_data = ((uint64_t)fc.inc_data_hi << 32) | fc.inc_data_lo;

@@ -115,6 +115,21 @@ def render_rgb8(scene, params, camera=None):
     return out, st
 
 
+def tile_order(scene, params, camera=None):
+    """rt_tile_order: the pass's 64-pixel blocks in dealing order as
+    (perm, n_lead, n_sky); perm is empty when the pass keeps the natural order."""
+    s, m = _scene_arrays(scene)
+    nb, nl, ns = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
+    args = (abi.ptr(s, C.POINTER(abi.RtSphere)), len(s), abi.ptr(m, C.POINTER(abi.RtMaterial)), len(m),
+            C.byref(_cam(camera, params)), C.byref(params))
+    check(lib().rt_tile_order(*args, None, 0, C.byref(nb), C.byref(nl), C.byref(ns)))
+    perm = np.zeros(nb.value, dtype=np.uint32)
+    if nb.value:
+        check(lib().rt_tile_order(*args, abi.ptr(perm, C.POINTER(C.c_uint32)), nb.value, C.byref(nb), C.byref(nl),
+                                  C.byref(ns)))
+    return perm, nl.value, ns.value
+
+
 def release_cached():
     """rt_release_cached: free the device context the synchronous renders keep between calls."""
     check(lib().rt_release_cached())

@@ -8,7 +8,7 @@
 namespace {
 // app::color (main.cxx:52-75) with a trace: returns the segment count; prim = kind of the
 // primary hit (0 sky, 1 lambert, 2 metal, 3 dielectric), fdi = segment (1-based) of the first
-// dielectric hit or 0
+// dielectric hit or 0; ground = a lambert hit below y = -0.05 (the huge scene's ground, top at y = -0.125)
 template <class G>
 std::uint32_t color_trace(const scene &sc, G &g, ray r, std::uint32_t depth, std::uint32_t &prim, std::uint32_t &fdi)
 {
@@ -20,7 +20,7 @@ std::uint32_t color_trace(const scene &sc, G &g, ray r, std::uint32_t depth, std
         hit h = hit_world(sc, r);
         if (!h.ok) return seg;
         const std::uint32_t kind = sc.m[h.mat].kind;
-        if (b == 0) prim = kind + 1;
+        if (b == 0) prim = kind + 1 + (kind == RT_LAMBERT && h.p.y < -0.05f ? 3u : 0u);
         if (kind == RT_DIELECTRIC && !fdi) fdi = seg;
         ray nr; v3 e;
         if (!apply_material(sc, g, r, h, nr, e)) return seg;

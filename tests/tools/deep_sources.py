@@ -70,9 +70,9 @@ def main():
     print(f"samples {n}, segments {int(segs.sum())} ({segs.sum() / n:.4f} per primary)")
     print(f"deep samples (> {args.split} segments): {nd} ({nd / n * 100:.4f}%), "
           f"reaching max depth: {int((segs >= args.depth).sum())}")
-    names = ["sky", "lambert", "metal", "dielectric"]
+    names = ["sky", "lambert sphere", "metal", "dielectric", "ground"]
     print("primary hit of the deep samples:",
-          ", ".join(f"{names[k]} {int((prim[deep] == k).sum())}" for k in range(4)))
+          ", ".join(f"{names[k]} {int((prim[deep] == k).sum())}" for k in range(5)))
     fd = fdi[deep]
     print("first dielectric hit of the deep samples: segment 1 %d, 2 %d, 3 %d, 4-8 %d, later %d, none %d" % (
         int((fd == 1).sum()), int((fd == 2).sum()), int((fd == 3).sum()), int(((fd >= 4) & (fd <= 8)).sum()),
@@ -82,10 +82,12 @@ def main():
     t = lambda a: a[:th * 8, :tw * 8].reshape(th, 8, tw, 8, *a.shape[2:]).swapaxes(1, 2).reshape(th, tw, -1)  # noqa: E731
     tp, tdeep, tseg = t(prim), t(deep), t(segs)
     has_d = (tp == 3).any(-1)
+    has_s = ((tp == 1) | (tp == 2)).any(-1)
     has_hit = (tp > 0).any(-1)
-    cls = np.where(has_d, 0, np.where(has_hit, 1, 2))
+    cls = np.where(has_d, 0, np.where(has_s, 1, np.where(has_hit, 2, 3)))
     print(f"8x8 tiles: {th * tw}")
-    for c, name in enumerate(["a primary hits a dielectric", "a primary hits something else", "every primary reaches the sky"]):
+    for c, name in enumerate(["a primary hits a dielectric", "a primary hits another small sphere",
+                              "primaries hit the ground only", "every primary reaches the sky"]):
         sel = cls == c
         print(f"  class {c} ({name}): {int(sel.sum())} tiles ({sel.mean() * 100:.1f}%), "
               f"segments {tseg[sel].sum() / segs.sum() * 100:.1f}% of the frame's, "

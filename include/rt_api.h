@@ -191,8 +191,9 @@ enum rt_diag {
                                           that plan that must not depend on timing             */
     RT_DIAG_NATURAL_ORDER = 1u << 14,   /* items dealt in the pixels' natural tile order (no
                                           tile classes, no sky path)           */
-    RT_DIAG_NO_SKY = 1u << 15           /* tile classes order the dealing, but samples of tiles
+    RT_DIAG_NO_SKY = 1u << 15,          /* tile classes order the dealing, but samples of tiles
                                           proven to reach the sky trace their segment          */
+    RT_DIAG_LONE_SPLIT = 1u << 16       /* split a lone pass dealt by tile classes as well      */
 };
 int rt_options_default(rt_options *out);
 /* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,

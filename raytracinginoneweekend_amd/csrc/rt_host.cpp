@@ -1060,7 +1060,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         uint32_t stats_waves = 0;  // the instrumented build: waves of the launch the counters cover
         // a lone pass dealt by tile classes is not split: its trapped paths start in its first
         // items and end inside the bulk of the launch
-        if (may_split && (n_samples >= O.deep_min_items || in_flight) && (in_flight || !ordered)) {
+        if (may_split && (n_samples >= O.deep_min_items || in_flight) &&
+            (in_flight || !ordered || (O.diag & RT_DIAG_LONE_SPLIT))) {
             const uint32_t rcap = deep_region_cap(n_samples), cap = 8u * rcap;
             const size_t px_bytes = deep_px_bytes(n_pixels);
             bool fresh = false;

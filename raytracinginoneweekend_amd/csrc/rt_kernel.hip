@@ -238,10 +238,27 @@ __device__ __forceinline__ uint32_t udiv(uint32_t n, const UD &u)
 
 // pixel (x, packed row rr) of enumeration position i; perm: the pass's block permutation
 // (KParams::block_perm) or null
+#ifndef RT_PERM_SCALAR
+#define RT_PERM_SCALAR 1  // A/B build switch: the block permutation read through the scalar cache
+#endif
 template <class FC>
 __device__ __forceinline__ void pixel_of(const FC &fc, uint32_t i, uint32_t &x, uint32_t &rr, const uint32_t *perm)
 {
-    if (perm) i = (perm[i >> 6] << 6) | (i & 63u);
+    if (perm) {
+        // the active lanes' positions lie in one or two blocks nearly always (fresh lanes take
+        // consecutive items of one tile at one sample): the first lane's block through a scalar
+        // load, vector loads only for lanes in another block
+        const uint32_t b = i >> 6;
+        uint32_t nb;
+        if (RT_PERM_SCALAR) {
+            const uint32_t b0 = __builtin_amdgcn_readfirstlane(b);
+            nb = perm[b0];
+            if (b != b0) nb = perm[b];
+        } else {
+            nb = perm[b];
+        }
+        i = (nb << 6) | (i & 63u);
+    }
     const uint32_t W = fc.W, tiled_rows = fc.tiled_rows, tiles_x = fc.tiles_x;
     const uint32_t tiled_px = tiled_rows * W;
     if (i < tiled_px) {
@@ -1890,9 +1907,13 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
         if (k.part == 2 && !flagged) return;
         if (k.part != 1 && flagged) k.deep_px[i] = 0;
     }
+    // i: the pixel's position in this pass's slots (its permuted enumeration);
+    // ni: its natural enumeration index, which indexes the running sums (passes of one frame may
+    // be dealt in different orders) and places the output
+    const uint32_t ni = k.block_perm ? (k.block_perm[i >> 6] << 6) | (i & 63u) : i;
     f3 acc;
     if (k.first) acc = mk(0.f, 0.f, 0.f);
-    else acc = mk(k.acc[3 * i], k.acc[3 * i + 1], k.acc[3 * i + 2]);
+    else acc = mk(k.acc[3 * ni], k.acc[3 * ni + 1], k.acc[3 * ni + 2]);
     // main.cxx:205 = libstdc++ reduce (<numeric>:443-460): ((c0+c1)+(c2+c3)) per block of 4,
     // blocks in order, then the spp % 4 tail one by one. Passes start on a multiple of 4.
     auto ld = [&](uint32_t s) {
@@ -1909,14 +1930,13 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
         for (; s < k.n_samples; ++s) acc = acc + ld(s);
     }
     if (!k.last) {
-        k.acc[3 * i] = acc.x; k.acc[3 * i + 1] = acc.y; k.acc[3 * i + 2] = acc.z;
+        k.acc[3 * ni] = acc.x; k.acc[3 * ni + 1] = acc.y; k.acc[3 * ni + 2] = acc.z;
         return;
     }
     const f3 col = acc / (float)k.spp;  // main.cxx:207
-    // output position (the slots' enumeration is the pass's permuted one)
+    // output position
     uint32_t x, rr;
     {
-        const uint32_t ni = k.block_perm ? (k.block_perm[i >> 6] << 6) | (i & 63u) : i;
         const uint32_t tiled_px = k.tiled_rows * k.W;
         if (ni < tiled_px) {
             uint32_t t = ni >> 6, w = ni & 63u;

@@ -592,6 +592,10 @@ int pass_order(rt_scene *sc, const rt_camera &cam, const rt::KParams &k, const r
     rt_scene::Order e;
     e.key.swap(key);
     e.t = classify_tiles(cam, k.W, k.H, k.row_offset, k.row_stride, k.num_rows, k.tile_lw, sc->geom);
+#ifdef RT_ORDER_IDENTITY  // A/B build switch: the class machinery over the natural order (one middle group)
+    for (uint32_t i = 0; i < e.t.perm.size(); ++i) e.t.perm[i] = i;
+    e.t.n_lead = e.t.n_sky = 0;
+#endif
     if (!e.t.perm.empty()) {
         RT_HIP(hipMalloc((void **)&e.d_perm, e.t.perm.size() * sizeof(uint32_t)));
         const hipError_t ce = hipMemcpy(e.d_perm, e.t.perm.data(), e.t.perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -1031,25 +1035,30 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.guided_l2b = guided_l2b(grid * 4u, in_flight);
         k.block_perm = nullptr;
         k.n_groups = 1;
-        k.sky_group = 0;
+        k.sky_slot = 0xffffffffu;
         k.grp_blocks[0] = k.n_blocks;
-        k.grp_items0 = k.n_items;
+        k.grp_slot[0] = 0;
+        k.grp_slot[1] = k.grp_slot[2] = k.grp_slot[3] = k.n_items;
+        k.grp_pix[0] = 0;
+        k.grp_pix[1] = k.grp_pix[2] = k.grp_pix[3] = k.n_pixels;
         if (ordered) {
             const rthost::tile_order &t = ord->t;
             const uint64_t S = s1 - s0;
             const uint64_t nbl[3] = {t.n_lead, t.perm.size() - t.n_lead - t.n_sky, t.n_sky};
             k.block_perm = ord->d_perm;
+#ifdef RT_ORDER_NULLPERM  // A/B build switch (with RT_ORDER_IDENTITY): the identity permutation not read
+            k.block_perm = nullptr;
+#endif
             k.n_groups = 3;
-            k.sky_group = (O.diag & RT_DIAG_NO_SKY) ? 0u : 1u;
-            k.grp_pix[0] = 0;
             for (int g = 0; g < 3; ++g) {
                 k.grp_pix[g + 1] = k.grp_pix[g] + static_cast<uint32_t>(64u * nbl[g]);
+                k.grp_slot[g + 1] = k.grp_slot[g] + static_cast<uint32_t>(64u * nbl[g] * S);
                 k.div_grp[g] = make_udiv(static_cast<uint32_t>(std::max<uint64_t>(64u * nbl[g], 1u)));
                 k.grp_blocks[g] = static_cast<uint32_t>(nbl[g] * S);  // nbl[g] blocks per sample
             }
-            k.grp_items0 = 64u * k.grp_blocks[0];
+            if (!(O.diag & RT_DIAG_NO_SKY) && nbl[2]) k.sky_slot = k.grp_slot[2];
             sc->used_lead = t.n_lead;
-            sc->used_sky = k.sky_group ? t.n_sky : 0u;
+            sc->used_sky = k.sky_slot != 0xffffffffu ? t.n_sky : 0u;
         } else {
             sc->used_lead = sc->used_sky = 0;
         }
@@ -1222,6 +1231,11 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         a.queue_reset = k.queue_ctr;
         a.queue_words = 8 * rt::kQueueStride;
         a.block_perm = k.block_perm;
+        a.n_groups = k.n_groups;
+        for (int g = 0; g < 4; ++g) {
+            a.grp_pix[g] = k.grp_pix[g];
+            a.grp_slot[g] = k.grp_slot[g];
+        }
         if (k.deep_depth) {
             a.deep_over = sc->deep_over_dev + wb;
             a.deep_key = deep_key;

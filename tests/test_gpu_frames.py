@@ -457,9 +457,10 @@ def test_lone_deep_launch_static_dealing_runs(opts):
     (8 | 16); frames in flight take the 4-wave launch (4). Both equal the unsplit render bit for
     bit, with the same segment counts (no test checked that the static path ran)."""
     torch = pytest.importorskip("torch")
-    opts.set(deep_min_items=0, shade_global=True)
+    # (lone_split: a lone pass dealt by tile classes is not split otherwise, DESIGN.md §4.7)
+    opts.set(deep_min_items=0, shade_global=True, lone_split=True)
     s, m = G.scene("huge")
-    W, H, spp = 640, 360, 64  # ~0.8 ms a frame: the next call arrives while it runs
+    W, H, spp = 640, 360, 64
     cam = rt.Camera.default(W, H)
     p = rt.make_params(W, H, spp, 64, 17)
     opts.set(deep_split=0)

@@ -135,21 +135,25 @@ struct KParams {
     uint32_t diag_unbounded_nb;
     // Dealing order. The pixel enumeration is permuted by 64-pixel blocks:
     // position i holds pixel (block_perm[i / 64] * 64 + i % 64) of the natural enumeration
-    // (identity when block_perm is null). The positions form n_groups groups [grp_pix[g],
-    // grp_pix[g + 1]): the lead tiles, the others, the sky tiles. A pass's slots are group-major,
-    // [group][sample][position in the group]: group g's items are slots [grp_slot[g], grp_slot[g +
-    // 1]), sample-major over its ng positions, and an item's index IS its slot. Each group is dealt
-    // from 8 queues, queue q owning the q-th eighth of the group's grp_blocks[g] blocks of 64 items;
-    // a queue's waves deal its share of group 0, then of group 1, then of group 2, and steal other
-    // queues' shares of the last group. One group (natural order): the pass's items as before.
+    // (identity when block_perm is null), and a pass's slots are [sample][position]. The
+    // positions form n_groups groups [grp_pix[g], grp_pix[g + 1]): the lead tiles, the others,
+    // the sky tiles. Group g's grp_items[g] items (sample-major over its positions, item J =
+    // sample J / ng, position grp_pix[g] + J % ng) are dealt from 8 queues, queue q owning the q-th
+    // eighth of its grp_blocks[g] blocks of 64; every wave deals group g from every queue before it
+    // takes group g + 1. One group (natural order): item J = slot J.
     const uint32_t *block_perm;
     uint32_t n_groups;          // 1: natural order, 3: tile classes
-    uint32_t sky_slot;          // the first slot of the proven sky tiles' group (~0: none)
+    uint32_t sky_grp;           // the group of the proven sky tiles (kItSky), 3 = none
     uint32_t grp_pix[4];
-    uint32_t grp_slot[4];
+    uint32_t grp_items[3];
     uint32_t grp_blocks[3];     // (natural order: n_blocks, the last one possibly partial)
     UDiv div_grp[3];            // division by group g's position count
 };
+
+// the main launch's item word (below kItSlot: the slot) of a pass dealt by tile classes: the
+// sample's tile is proven to send every primary ray to the sky (single samples only: the pair
+// instantiation uses this bit as kItFirstDeep)
+constexpr uint32_t kItSky = 1u << 30;
 
 // V_STATS_LDS: every lane-computed index into the scene blob, the slots and the deep queue is
 // checked against its bound before use; the first violation is recorded in dbg[kDbgError] as
@@ -186,8 +190,6 @@ struct KAccum {
     unsigned long long deep_key;
     uint32_t deep_rcap;
     const uint32_t *block_perm;  // the pass's permuted enumeration (KParams::block_perm), or null
-    uint32_t n_groups;           // KParams::n_groups: 3 = group-major slots (grp_pix, grp_slot)
-    uint32_t grp_pix[4], grp_slot[4];
     // split passes accumulate in two parts: part 1 (after the main launch, beside the deep one)
     // the pixels none of whose samples went to the deep queue, part 2 (after the deep launch)
     // the others, clearing their flags; part 3 (caller stream only): every pixel, clearing the

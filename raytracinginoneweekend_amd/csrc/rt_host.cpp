@@ -1035,12 +1035,12 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.guided_l2b = guided_l2b(grid * 4u, in_flight);
         k.block_perm = nullptr;
         k.n_groups = 1;
-        k.sky_slot = 0xffffffffu;
+        k.sky_grp = 3;
         k.grp_blocks[0] = k.n_blocks;
-        k.grp_slot[0] = 0;
-        k.grp_slot[1] = k.grp_slot[2] = k.grp_slot[3] = k.n_items;
+        k.grp_items[0] = k.n_items;
         k.grp_pix[0] = 0;
         k.grp_pix[1] = k.grp_pix[2] = k.grp_pix[3] = k.n_pixels;
+        k.div_grp[0] = make_udiv(k.n_pixels);
         if (ordered) {
             const rthost::tile_order &t = ord->t;
             const uint64_t S = s1 - s0;
@@ -1052,13 +1052,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             k.n_groups = 3;
             for (int g = 0; g < 3; ++g) {
                 k.grp_pix[g + 1] = k.grp_pix[g] + static_cast<uint32_t>(64u * nbl[g]);
-                k.grp_slot[g + 1] = k.grp_slot[g] + static_cast<uint32_t>(64u * nbl[g] * S);
-                k.div_grp[g] = make_udiv(static_cast<uint32_t>(std::max<uint64_t>(64u * nbl[g], 1u)));
+                k.grp_items[g] = static_cast<uint32_t>(64u * nbl[g] * S);
                 k.grp_blocks[g] = static_cast<uint32_t>(nbl[g] * S);  // nbl[g] blocks per sample
+                k.div_grp[g] = make_udiv(static_cast<uint32_t>(std::max<uint64_t>(64u * nbl[g], 1u)));
             }
-            if (!(O.diag & RT_DIAG_NO_SKY) && nbl[2]) k.sky_slot = k.grp_slot[2];
+            if (!(O.diag & RT_DIAG_NO_SKY) && nbl[2]) k.sky_grp = 2;
             sc->used_lead = t.n_lead;
-            sc->used_sky = k.sky_slot != 0xffffffffu ? t.n_sky : 0u;
+            sc->used_sky = k.sky_grp == 2 ? t.n_sky : 0u;
         } else {
             sc->used_lead = sc->used_sky = 0;
         }
@@ -1231,11 +1231,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         a.queue_reset = k.queue_ctr;
         a.queue_words = 8 * rt::kQueueStride;
         a.block_perm = k.block_perm;
-        a.n_groups = k.n_groups;
-        for (int g = 0; g < 4; ++g) {
-            a.grp_pix[g] = k.grp_pix[g];
-            a.grp_slot[g] = k.grp_slot[g];
-        }
         if (k.deep_depth) {
             a.deep_over = sc->deep_over_dev + wb;
             a.deep_key = deep_key;

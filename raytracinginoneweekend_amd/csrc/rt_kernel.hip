@@ -969,6 +969,9 @@ __device__ __forceinline__ void render_body(const KParams &p)
     // order of the regions' chunks; the grid's waves take chunks w, w + waves, w + 2 waves, ...
     uint32_t deep_next = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + (threadIdx.x >> 6));
     uint32_t cnext = 0, cend = 0;
+    // the main launch: the chunk's items [cnext, run_end) lie in one sample, at slots run_base + ...
+    uint32_t run_end = 0, run_base = 0;
+    bool run_sky = false;  // ... of the proven sky tiles (kItSky)
     bool exhausted = false;
 
     // lane state: the lane's item is one sample (pixel enumeration index, sample of the pass)
@@ -1051,6 +1054,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
             RT_EV(EV_REFILL_TRIP);
+            if (!DEEP && cnext < cend && cnext >= run_end) goto run;  // the chunk's next sample
             if (cnext >= cend) {
                 uint32_t c = 0;
                 if constexpr (DEEP) {
@@ -1100,17 +1104,15 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 const uint32_t grp = q >> 3, qq = q & 7u;
                 if (lane == 0) c = atomicAdd(P.queue_ctr + qq * kQueueStride + grp, 1u);  // word grp of queue qq's line
                 c = __builtin_amdgcn_readfirstlane(c);
-                // guided: queue q owns blocks [qb0, qb1) of 64 items of the group; ticket c takes blocks
+                // guided: queue q owns blocks [qb0, qb1) of 64 items of the group (group-local
+                // indices, KParams::n_groups); ticket c takes blocks
                 // [S(c), S(c+1)), S(t) = min(B, floor(B (1 - beta^t)) + 2t): chunks shrink
                 // geometrically from ~B / (K waves per queue) to 2 blocks, so a queue is
                 // served by few atomics and its last chunks are small. S is the same
                 // function for every wave, so consecutive tickets tile the range; the 2t
                 // term keeps it increasing even if exp2 or the float product is off by an
                 // ulp (one block at most).
-                // the group's item blocks, an eighth per queue (group-local)
                 const uint32_t GB = grp == 0u ? P.grp_blocks[0] : grp == 1u ? P.grp_blocks[1] : P.grp_blocks[2];
-                const uint32_t g0 = grp == 0u ? 0u : grp == 1u ? P.grp_slot[1] : P.grp_slot[2];
-                const uint32_t g1 = grp == 0u ? P.grp_slot[1] : grp == 1u ? P.grp_slot[2] : P.grp_slot[3];
                 const uint32_t qb0 = (uint32_t)(((uint64_t)GB * qq) >> 3);
                 const uint32_t B = (uint32_t)(((uint64_t)GB * (qq + 1u)) >> 3) - qb0;
                 auto S = [&](uint32_t t) -> uint32_t {
@@ -1120,25 +1122,44 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 };
                 const uint32_t s0 = __builtin_amdgcn_readfirstlane(S(c));
                 if (s0 >= B) {
-                    if (grp + 1u < P.n_groups) {
-                        q += 8u;  // this queue's share of the next group
-                    } else {
-                        // the last group: the other queues' shares, then done
-                        q = (q & ~7u) | ((q + 1u) & 7u);
-                        if (++q_tried == 8u) exhausted = true;
+                    // the group's next queue; after all 8, the next group (a group is dealt
+                    // whole, by every wave, before the next one starts)
+                    q = (q & ~7u) | ((q + 1u) & 7u);
+                    if (++q_tried == 8u) {
+                        q_tried = 0;
+                        q += 8u;
+                        if (q >= 8u * P.n_groups) exhausted = true;
                     }
                     continue;
                 }
-                cnext = g0 + 64u * (qb0 + s0);  // items are slots (group-major)
-                cend = __builtin_amdgcn_readfirstlane(min(g0 + 64u * (qb0 + S(c + 1u)), g1));
+                const uint32_t GI = grp == 0u ? P.grp_items[0] : grp == 1u ? P.grp_items[1] : P.grp_items[2];
+                cnext = 64u * (qb0 + s0);
+                cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), GI));
                 }
             }
+        run:
+            if constexpr (!DEEP) {
+                // the chunk's run within one sample: group grp's item J is sample J / ng at
+                // position p0 + J % ng, slot [sample][position] (sample-major over the pass's
+                // permuted enumeration); one group (natural order): slot J
+                const uint32_t grp = q >> 3;
+                const uint32_t p0 = grp == 0u ? 0u : grp == 1u ? P.grp_pix[1] : P.grp_pix[2];
+                const uint32_t ng = (grp == 0u ? P.grp_pix[1] : grp == 1u ? P.grp_pix[2] : P.grp_pix[3]) - p0;
+                UDiv dv;
+                dv.m = grp == 0u ? P.div_grp[0].m : grp == 1u ? P.div_grp[1].m : P.div_grp[2].m;
+                dv.s1 = grp == 0u ? P.div_grp[0].s1 : grp == 1u ? P.div_grp[1].s1 : P.div_grp[2].s1;
+                dv.s2 = grp == 0u ? P.div_grp[0].s2 : grp == 1u ? P.div_grp[1].s2 : P.div_grp[2].s2;
+                const uint32_t sj = __builtin_amdgcn_readfirstlane(udiv(cnext, dv));
+                run_end = __builtin_amdgcn_readfirstlane(min(cend, (sj + 1u) * ng));
+                run_base = __builtin_amdgcn_readfirstlane(sj * P.n_pixels + p0 + (cnext - sj * ng));
+                run_sky = grp == P.sky_grp;
+            }
         deal:
-            const uint32_t avail = cend - cnext;
+            const uint32_t avail = (DEEP ? cend : run_end) - cnext;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (!alive && rank < avail) {
-                uint32_t I = cnext + rank;
+                uint32_t I = (DEEP ? cnext : run_base) + rank;
                 if constexpr (DEEP) {
                     // a queued path resumes where the main launch left it: the ray of its next
                     // segment, attenuation, data stream and segment count; ls = 0 and pix = the
@@ -1177,12 +1198,14 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     HID(sl) = hid;
                 } else {
                     it = I;  // a pair item (the pass's full blocks) or a single tail sample; its slot
+                    if (!PAIRS && run_sky) it |= kItSky;
                     alive = fresh = true;
                 }
             }
             const uint32_t took = min((uint32_t)__popcll(need), avail);
             if (STATS) dbg_dealt += took;
             cnext += took;
+            if (!DEEP) run_base += took;
             need = ballot(!alive);
         }
 
@@ -1202,36 +1225,6 @@ __device__ __forceinline__ void render_body(const KParams &p)
         // the pixel (enumeration index) and the sample of the pass of the lane's item word
         auto item_pixel = [&](uint32_t &s) -> uint32_t {
             const uint32_t sl = it & kItSlot;
-            if (!PAIRS && P.n_groups > 1u) {
-                // group-major slots: group g holds slots [grp_slot[g], grp_slot[g + 1]),
-                // sample-major over its positions; a wave's lanes are nearly always in one group
-                const uint32_t g = (sl >= P.grp_slot[1] ? 1u : 0u) + (sl >= P.grp_slot[2] ? 1u : 0u);
-                const uint32_t gu = __builtin_amdgcn_readfirstlane(g);
-                uint32_t J, ng, p0, q;
-                if (!ballot(g != gu)) {
-                    const uint32_t b0 = gu == 0u ? 0u : gu == 1u ? P.grp_slot[1] : P.grp_slot[2];
-                    p0 = gu == 0u ? 0u : gu == 1u ? P.grp_pix[1] : P.grp_pix[2];
-                    ng = (gu == 0u ? P.grp_pix[1] : gu == 1u ? P.grp_pix[2] : P.grp_pix[3]) - p0;
-                    UDiv dv;
-                    dv.m = gu == 0u ? P.div_grp[0].m : gu == 1u ? P.div_grp[1].m : P.div_grp[2].m;
-                    dv.s1 = gu == 0u ? P.div_grp[0].s1 : gu == 1u ? P.div_grp[1].s1 : P.div_grp[2].s1;
-                    dv.s2 = gu == 0u ? P.div_grp[0].s2 : gu == 1u ? P.div_grp[1].s2 : P.div_grp[2].s2;
-                    J = sl - b0;
-                    q = udiv(J, dv);
-                } else {
-                    const uint32_t b0 = g == 0u ? 0u : g == 1u ? P.grp_slot[1] : P.grp_slot[2];
-                    p0 = g == 0u ? 0u : g == 1u ? P.grp_pix[1] : P.grp_pix[2];
-                    ng = (g == 0u ? P.grp_pix[1] : g == 1u ? P.grp_pix[2] : P.grp_pix[3]) - p0;
-                    UDiv dv;
-                    dv.m = g == 0u ? P.div_grp[0].m : g == 1u ? P.div_grp[1].m : P.div_grp[2].m;
-                    dv.s1 = g == 0u ? P.div_grp[0].s1 : g == 1u ? P.div_grp[1].s1 : P.div_grp[2].s1;
-                    dv.s2 = g == 0u ? P.div_grp[0].s2 : g == 1u ? P.div_grp[1].s2 : P.div_grp[2].s2;
-                    J = sl - b0;
-                    q = udiv(J, dv);
-                }
-                s = q;
-                return p0 + J - q * ng;
-            }
             const uint32_t npi = PAIRS ? (uint32_t)P.n_pair_items : 0u;
             const bool pr = sl < npi;
             const uint32_t J = pr ? sl : sl - npi;
@@ -1489,11 +1482,11 @@ __device__ __forceinline__ void render_body(const KParams &p)
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && !defer && depth < P.max_depth;  // depth check: main.cxx:74
         // the segments that test spheres: all but the primary rays of the tiles proven to send
-        // every primary ray to the sky (slots from KParams::sky_slot), whose segment meets no sphere:
+        // every primary ray to the sky (kItSky), whose segment meets no sphere:
         // they skip the closest-hit test and take the sky colour directly (a wave of them alone
         // runs no test at all; beside other lanes, they neither walk nor find a candidate in the
         // always-tested spheres, by the same proof)
-        auto sky_ray = [&]() { return !DEEP && !PAIRS && depth == 0u && (it & kItSlot) >= P.sky_slot; };
+        auto sky_ray = [&]() { return !DEEP && !PAIRS && depth == 0u && (it & kItSky) != 0u; };
         // |d|^2 (raytracer.hxx:56) and its refined reciprocal for this segment's roots; the sky
         // below reuses both (unit_direction's length is sqrt of the same sum)
         const float a = d.x * d.x + d.y * d.y + d.z * d.z;
@@ -1935,17 +1928,8 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
     else acc = mk(k.acc[3 * ni], k.acc[3 * ni + 1], k.acc[3 * ni + 2]);
     // main.cxx:205 = libstdc++ reduce (<numeric>:443-460): ((c0+c1)+(c2+c3)) per block of 4,
     // blocks in order, then the spp % 4 tail one by one. Passes start on a multiple of 4.
-    // sample s of this pixel: slot s n_pixels + i, or in group-major slots group
-    // g's slot grp_slot[g] + s ng + (i - grp_pix[g])
-    uint32_t base = i, stride = k.n_pixels;
-    if (k.n_groups > 1u) {
-        const uint32_t g = (i >= k.grp_pix[1] ? 1u : 0u) + (i >= k.grp_pix[2] ? 1u : 0u);
-        const uint32_t p0 = g == 0u ? 0u : g == 1u ? k.grp_pix[1] : k.grp_pix[2];
-        stride = (g == 0u ? k.grp_pix[1] : g == 1u ? k.grp_pix[2] : k.grp_pix[3]) - p0;
-        base = (g == 0u ? 0u : g == 1u ? k.grp_slot[1] : k.grp_slot[2]) + (i - p0);
-    }
     auto ld = [&](uint32_t s) {
-        const float *v = k.slots + ((size_t)s * stride + base) * 3u;
+        const float *v = k.slots + ((size_t)s * k.n_pixels + i) * 3u;
         return mk(v[0], v[1], v[2]);
     };
     if (k.paired) {

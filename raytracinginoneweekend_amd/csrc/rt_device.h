@@ -190,6 +190,9 @@ struct KAccum {
     unsigned long long deep_key;
     uint32_t deep_rcap;
     const uint32_t *block_perm;  // the pass's permuted enumeration (KParams::block_perm), or null
+    // positions from sky_pos0 on are the sky kernel's (n_pixels: none): skipped by every pass but
+    // the last, whose accumulation divides their sums (at their sample-0 slots) by spp
+    uint32_t sky_pos0;
     // split passes accumulate in two parts: part 1 (after the main launch, beside the deep one)
     // the pixels none of whose samples went to the deep queue, part 2 (after the deep launch)
     // the others, clearing their flags; part 3 (caller stream only): every pixel, clearing the
@@ -211,6 +214,17 @@ struct KCompat {
     float *out;
     uint32_t *ctr;
     unsigned long long *segments;  // optional [3]: segments, sphere tests, 0
+};
+
+// The sky kernel: every sample of the pixels of the tiles proven to send every
+// primary ray to the sky, one thread per pixel, its samples summed in the reference's blocked
+// order (main.cxx:205); sky position i's sum (not yet divided by spp) goes to sums[i - pos0].
+struct KSky {
+    FrameConsts fc;                // the frame (all of its samples: fc.spp; fc.sample_begin unused)
+    const uint32_t *block_perm;
+    uint32_t pos0, n_pix;          // the sky positions [pos0, pos0 + n_pix) of the enumeration
+    float *sums;
+    unsigned long long *segments;  // optional: adds n_pix * spp segments (no sphere test)
 };
 
 // The wavefront variant's ray queue (structure of arrays, capacity cap rays): f = [9][cap]

@@ -43,6 +43,7 @@ hipError_t launch_wave_bounce(int cull, const KWave &w, uint32_t grid, hipStream
 hipError_t occupancy_wave_bounce(int cull, int *blocks_per_cu, size_t lds);
 hipError_t occupancy_compat(int *blocks_per_cu);
 hipError_t launch_epilogue(const float *in, uint8_t *out, uint64_t n, hipStream_t stream);
+hipError_t launch_sky(const KSky &k, hipStream_t stream);
 } // namespace rt
 
 namespace {
@@ -982,6 +983,14 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         wgrid = ow * sc->cu_count;
     }
 
+    // the frame's dealing order (not with sample pairs) and the sky kernel: the
+    // tiles proven to send every primary ray to the sky are rendered by sky_kernel at the frame's
+    // last pass (all samples, one thread per pixel, no slots), the passes deal the others
+    const rt_scene::Order *ord = nullptr;
+    if (order_ok && !pairs)
+        if (int rc = pass_order(sc, *camera, k, &ord); rc) return rc;
+    const bool sky_kernel = ord && ord->d_perm && ord->t.n_sky && !(O.diag & (RT_DIAG_NO_SKY | RT_DIAG_SKY_IN_MAIN));
+    const uint32_t sky_pos0 = sky_kernel ? static_cast<uint32_t>(64u * (ord->t.perm.size() - ord->t.n_sky)) : k.n_pixels;
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
     auto others_running = [&] { return pipe && sc->last_ws >= 0 && hipEventQuery(sc->ev_done[sc->last_ws]) == hipErrorNotReady; };
@@ -1019,16 +1028,15 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.sample_end = s1;
         k.n_pair_items = static_cast<uint32_t>(((s1 - s0) - slot_rows(s0, s1, pass_pairs)) * n_pixels);
         if (k.n_pair_items) ++sc->used_pairs;
-        // dealing order: lead tiles first and proven sky tiles last in every
-        // queue's share (single-sample passes of the culled LDS kernels), else the natural order
-        const rt_scene::Order *ord = nullptr;
-        if (order_ok && !k.n_pair_items)
-            if (int rc = pass_order(sc, *camera, k, &ord); rc) return rc;
-        const bool ordered = ord && ord->d_perm;
+        // dealing order: lead tiles first, then the others (then the proven sky
+        // tiles, unless the sky kernel renders them) in single-sample passes of the culled LDS
+        // kernels, else the natural order
+        const bool ordered = ord && ord->d_perm && !k.n_pair_items;
         fill_frame_consts(k);
-        // items: the pass's pair items and its single tail samples (one slot each)
+        // items: the pass's pair items and its single tail samples (one slot each); with the sky
+        // kernel, the positions before the sky tiles'
         const uint64_t n_samples = n_pixels * (s1 - s0);
-        k.n_items = static_cast<uint32_t>(n_pixels * slot_rows(s0, s1, pass_pairs));
+        k.n_items = static_cast<uint32_t>((ordered && sky_kernel ? sky_pos0 : n_pixels) * slot_rows(s0, s1, pass_pairs));
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(pass_pairs ? occ_pr : occ, in_flight, bufs, n_samples)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
@@ -1044,12 +1052,12 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         if (ordered) {
             const rthost::tile_order &t = ord->t;
             const uint64_t S = s1 - s0;
-            const uint64_t nbl[3] = {t.n_lead, t.perm.size() - t.n_lead - t.n_sky, t.n_sky};
+            const uint64_t nbl[3] = {t.n_lead, t.perm.size() - t.n_lead - t.n_sky, sky_kernel ? 0u : t.n_sky};
             k.block_perm = ord->d_perm;
 #ifdef RT_ORDER_NULLPERM  // A/B build switch (with RT_ORDER_IDENTITY): the identity permutation not read
             k.block_perm = nullptr;
 #endif
-            k.n_groups = 3;
+            k.n_groups = sky_kernel ? 2 : 3;
             for (int g = 0; g < 3; ++g) {
                 k.grp_pix[g + 1] = k.grp_pix[g] + static_cast<uint32_t>(64u * nbl[g]);
                 k.grp_items[g] = static_cast<uint32_t>(64u * nbl[g] * S);
@@ -1058,7 +1066,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             }
             if (!(O.diag & RT_DIAG_NO_SKY) && nbl[2]) k.sky_grp = 2;
             sc->used_lead = t.n_lead;
-            sc->used_sky = k.sky_grp == 2 ? t.n_sky : 0u;
+            sc->used_sky = k.sky_grp == 2 || sky_kernel ? t.n_sky : 0u;
         } else {
             sc->used_lead = sc->used_sky = 0;
         }
@@ -1202,6 +1210,18 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) stats_waves = dgrid * static_cast<uint32_t>(wpb);
             }
         }
+        if (sky_kernel && s1 == P.spp) {
+            // the sky tiles' pixels, every sample of the frame; position i's sum to its sample-0
+            // slot (which no pass of these groups uses), read by this pass's accumulation
+            rt::KSky ks{};
+            ks.fc = k.fc;
+            ks.block_perm = k.block_perm;
+            ks.pos0 = sky_pos0;
+            ks.n_pix = k.n_pixels - sky_pos0;
+            ks.sums = k.slots + 3u * static_cast<size_t>(sky_pos0);
+            ks.segments = k.segments;
+            RT_HIP(rt::launch_sky(ks, xst));
+        }
         if (variant == rt::V_STATS_LDS) sc->dbg_waves = stats_waves;
         if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], xst));
         if (pipe) {
@@ -1231,6 +1251,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         a.queue_reset = k.queue_ctr;
         a.queue_words = 8 * rt::kQueueStride;
         a.block_perm = k.block_perm;
+        a.sky_pos0 = sky_pos0;
         if (k.deep_depth) {
             a.deep_over = sc->deep_over_dev + wb;
             a.deep_key = deep_key;

@@ -1913,7 +1913,12 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
     if (i >= k.n_pixels) return;
     // split passes (KAccum::part): 1 = pixels without deep samples, 2 = the others, 3 = all
     // pixels in one part; 2 and 3 clear the flags for the workspace's next pass
-    if (k.part) {
+    // the sky kernel's pixels: their sums wait at their sample-0 slots for the
+    // frame's last pass, after the sky kernel (not in part 1, which runs beside the deep launch)
+    const bool sky = i >= k.sky_pos0;
+    if (sky) {
+        if (!k.last || k.part == 1) return;
+    } else if (k.part) {
         const bool flagged = k.deep_px[i];
         if (k.part == 1 && flagged) return;
         if (k.part == 2 && !flagged) return;
@@ -1924,7 +1929,8 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
     // be dealt in different orders) and places the output
     const uint32_t ni = k.block_perm ? (k.block_perm[i >> 6] << 6) | (i & 63u) : i;
     f3 acc;
-    if (k.first) acc = mk(0.f, 0.f, 0.f);
+    if (sky) acc = mk(k.slots[3 * i], k.slots[3 * i + 1], k.slots[3 * i + 2]);
+    else if (k.first) acc = mk(0.f, 0.f, 0.f);
     else acc = mk(k.acc[3 * ni], k.acc[3 * ni + 1], k.acc[3 * ni + 2]);
     // main.cxx:205 = libstdc++ reduce (<numeric>:443-460): ((c0+c1)+(c2+c3)) per block of 4,
     // blocks in order, then the spp % 4 tail one by one. Passes start on a multiple of 4.
@@ -1932,7 +1938,9 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
         const float *v = k.slots + ((size_t)s * k.n_pixels + i) * 3u;
         return mk(v[0], v[1], v[2]);
     };
-    if (k.paired) {
+    if (sky) {
+        // (summed by sky_kernel over every sample of the frame)
+    } else if (k.paired) {
         // pair sums: slot 2b holds c0+c1, slot 2b+1 c2+c3 of block b; then the tail's samples
         for (uint32_t b = 0; b < k.n_blocks; ++b) acc = acc + (ld(2u * b) + ld(2u * b + 1u));
         for (uint32_t t = 4u * k.n_blocks; t < k.n_samples; ++t) acc = acc + ld(t - 2u * k.n_blocks);
@@ -1972,6 +1980,84 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
         k.out_u8[o] = (uint8_t)(255.f * (float)pow((double)col.x, g));
         k.out_u8[o + 1] = (uint8_t)(255.f * (float)pow((double)col.y, g));
         k.out_u8[o + 2] = (uint8_t)(255.f * (float)pow((double)col.z, g));
+    }
+}
+
+// ---- the sky kernel -----------------------------------------------------
+// One thread per pixel of the tiles proven to send every primary ray to the sky: each sample is
+// the reference's primary ray (main.cxx:192-200, camera.hxx:46-57) and its colour the sky's
+// (main.cxx:71: background(.5 unit_direction(d).y + 1) times an attenuation of 1, exact), the
+// closest hit being proven empty. The lane's samples are summed in the blocked order of
+// main.cxx:205's std::reduce ((c0 + c1) + (c2 + c3) per block of 4, blocks in order, then the
+// tail), which accumulate_kernel then divides by spp. A lane makes at most RT_REJECT_CAP attempts
+// of its lens draw per iteration and resumes the same sequence in the next, so the wave does not
+// wait for its unluckiest lane's whole rejection run; same draws, same order, same bits.
+__global__ __launch_bounds__(256) void sky_kernel(const KSky p)
+{
+    const FrameConsts &fc = p.fc;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    const bool live = t < p.n_pix;
+    uint32_t px, rr;
+    pixel_of(fc, p.pos0 + (live ? t : 0u), px, rr, p.block_perm);
+    const uint32_t py = fc.row_offset + rr * fc.row_stride;
+    const uint64_t inc_data = ((uint64_t)fc.inc_data_hi << 32) | fc.inc_data_lo;
+    const uint64_t inc_cam = ((uint64_t)fc.inc_cam_hi << 32) | fc.inc_cam_lo;
+    const uint64_t key0 = (uint64_t)(py * fc.W + px) * fc.spp;
+    const uint32_t spp = fc.spp, full_end = spp & ~3u;
+    const float fW = fc.fW, fH = fc.fH, rW = fc.rW, rH = fc.rH;
+    const bool dw = fc.div_fast & 1u, dh = fc.div_fast & 2u;
+    const f3 org = mk(fc.org[0], fc.org[1], fc.org[2]), llc = mk(fc.llc[0], fc.llc[1], fc.llc[2]);
+    const f3 hor = mk(fc.hor[0], fc.hor[1], fc.hor[2]), ver = mk(fc.ver[0], fc.ver[1], fc.ver[2]);
+    f3 acc = mk(0.f, 0.f, 0.f), part = acc, c2 = acc;
+    uint32_t s = live ? 0u : spp;
+    bool started = false;
+    uint64_t rc = 0;
+    float uu = 0.f, vv = 0.f;
+    Dbg dbg{};
+    while (ballot(s < spp)) {
+        if (s < spp) {
+            if (!started) {  // main.cxx:192-200 for sample s; key = (y W + x) spp + s
+                const uint64_t km = (key0 + s) * kPcgMul;
+                uint64_t rng = km + inc_data * (kPcgMul + 1u);
+                rc = km + inc_cam * (kPcgMul + 1u);
+                const float xu = canonical(rng, inc_data);
+                const float xv = canonical(rng, inc_data);
+                uu = div_const((float)px, fW, rW, dw) + div_const(xu, fW, rW, dw);
+                vv = div_const((float)py, fH, rH, dh) + div_const(xv, fH, rH, dh);
+                started = true;
+            }
+            bool got;
+            const f3 r = random_in_unit_sphere_capped<false>(rc, inc_cam, got, dbg);  // camera.hxx:52
+            if (got) {
+                const f3 rd = r * fc.lens;                                          // camera.hxx:46-57
+                const f3 off = mk(uu * rd.x, vv * rd.y, 0.f);
+                f3 d = ((llc + hor * uu) + ver * (1.f - vv)) - off;
+                if (fc.corrected) d = d - org;
+                const float tt = .5f * normalize(d).y + 1.f;                        // main.cxx:71
+                const f3 col = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
+                if (s < full_end) {
+                    const uint32_t j = s & 3u;
+                    if (j == 0u) part = col;
+                    else if (j == 1u) part = part + col;                            // c0 + c1
+                    else if (j == 2u) c2 = col;
+                    else acc = acc + (part + (c2 + col));                           // + ((c0+c1)+(c2+c3))
+                } else {
+                    acc = acc + col;                                                // the tail
+                }
+                ++s;
+                started = false;
+            }
+        }
+    }
+    if (live) {
+        float *o = p.sums + 3u * (size_t)t;
+        o[0] = acc.x;
+        o[1] = acc.y;
+        o[2] = acc.z;
+    }
+    if (p.segments) {
+        const uint32_t n = lanes(live);
+        if ((threadIdx.x & 63u) == 0u && n) atomicAdd(p.segments, (unsigned long long)n * spp);
     }
 }
 
@@ -2324,6 +2410,13 @@ hipError_t launch_accumulate(const KAccum &k, hipStream_t stream)
 {
     const uint32_t grid = (k.n_pixels + 255u) / 256u;
     hipLaunchKernelGGL(accumulate_kernel, dim3(grid), dim3(256), 0, stream, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_sky(const KSky &k, hipStream_t stream)
+{
+    if (!k.n_pix) return hipSuccess;
+    hipLaunchKernelGGL(sky_kernel, dim3((k.n_pix + 255u) / 256u), dim3(256), 0, stream, k);
     return hipGetLastError();
 }
 

@@ -695,15 +695,16 @@ def test_scene_at_the_lds_limit_renders_or_is_refused():
         _bits_equal(got, want, "culled at the LDS limit")
 
 
-@pytest.mark.parametrize("order", ["classes", "no_sky", "natural_order"])
+@pytest.mark.parametrize("order", ["classes", "sky_in_main", "no_sky", "natural_order"])
 def test_dealing_orders_keep_the_bits(order, opts):
-    """Passes dealt by tile classes (lead tiles first, proven sky tiles last, their
-    samples without a closest-hit test), by tile classes with the sky tiles traced, and in the
-    natural order render the same bits as the oracle: a lone frame (not split), frames in flight
-    (split, ring passes), an interleaved row share, fast-math against its own natural order, and
-    the corrected camera. rt_scene_usage reports the classes that were used."""
+    """Passes dealt by tile classes (lead tiles first; the proven sky tiles by the
+    sky kernel, or dealt last by the main launch without a closest-hit test, or traced), and in
+    the natural order render the same bits as the oracle: a lone frame (not split), frames in
+    flight (split, ring passes), an interleaved row share, fast-math against its own natural
+    order, and the corrected camera. rt_scene_usage reports the classes that were used."""
     torch = pytest.importorskip("torch")
-    diag = {"classes": {}, "no_sky": dict(no_sky=True), "natural_order": dict(natural_order=True)}[order]
+    diag = {"classes": {}, "sky_in_main": dict(sky_in_main=True), "no_sky": dict(no_sky=True),
+            "natural_order": dict(natural_order=True)}[order]
     opts.set(deep_min_items=0, **diag)
     s, m = G.scene("huge")
     stream = torch.cuda.current_stream().cuda_stream
@@ -727,7 +728,7 @@ def test_dealing_orders_keep_the_bits(order, opts):
             assert u["lead_tiles"] == 0 and u["sky_tiles"] == 0, u
         elif mode == 0:
             assert u["lead_tiles"] > 0, u
-            assert (u["sky_tiles"] > 0) == (order == "classes"), u
+            assert (u["sky_tiles"] > 0) == (order in ("classes", "sky_in_main")), u
     # the lone 320x176 frame is not split when dealt by classes
     assert (used[0]["split_passes"] == 0) == (order != "natural_order"), used[0]
     # fast-math: the classes and the sky path change no bit of its own result either

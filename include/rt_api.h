@@ -194,8 +194,10 @@ enum rt_diag {
     RT_DIAG_NO_SKY = 1u << 15,          /* tile classes order the dealing, but samples of tiles
                                           proven to reach the sky trace their segment          */
     RT_DIAG_LONE_SPLIT = 1u << 16,      /* split a lone pass dealt by tile classes as well      */
-    RT_DIAG_SKY_IN_MAIN = 1u << 17      /* the proven sky tiles dealt last by the main launch
+    RT_DIAG_SKY_IN_MAIN = 1u << 17,     /* the proven sky tiles dealt last by the main launch
                                           (no closest hit) instead of the sky kernel            */
+    RT_DIAG_SKY_SERIAL = 1u << 18       /* a lone pass's sky kernel after its main and deep
+                                          launches on their stream (not beside them)           */
 };
 int rt_options_default(rt_options *out);
 /* Applies "key=value[,key=value...]" (fields above; diag bits as ieee_roots, no_shortcut,

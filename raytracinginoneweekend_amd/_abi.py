@@ -81,7 +81,7 @@ RT_DIAG = {
     "shade_lds": 1 << 4, "shade_global": 1 << 5, "stats": 1 << 6, "stats_deep_only": 1 << 7, "verbose": 1 << 8,
     "standin_transport": 1 << 9, "unbounded_nb": 1 << 10, "no_pairs": 1 << 11, "pairs": 1 << 12,
     "in_flight": 1 << 13, "natural_order": 1 << 14, "no_sky": 1 << 15, "lone_split": 1 << 16,
-    "sky_in_main": 1 << 17,
+    "sky_in_main": 1 << 17, "sky_serial": 1 << 18,
 }
 
 

@@ -93,6 +93,7 @@ struct KParams {
     uint32_t tile_lw;                       // log2 of the tile width (3: 8x8, 4: 16x4, 5: 32x2, 6: 64x1)
     uint32_t sample_begin, sample_end;      // this launch's samples
     uint32_t n_items;
+    uint32_t n_slots;        // the pass's slots (bounds check): its slot rows x n_pixels (items may be fewer)
     uint32_t n_pair_items;   // items [0, n_pair_items) are sample pairs (FrameConsts::n_pairs x n_pixels),
                              // the rest single tail samples; the slot of item I is slot I either way
     uint32_t n_blocks;       // guided dealing: ceil(n_items / 64) blocks, 1/8 per queue

@@ -163,6 +163,10 @@ struct rt_scene {
     hipStream_t xs[kMaxBufs] = {};
     hipEvent_t ev_done[kMaxWs] = {}, ev_free[kMaxWs] = {};
     hipEvent_t ev_main[kMaxWs] = {};  // split passes: after the main launch (created on first use)
+    // the sky kernel of a pass issued alone runs on a stream of its own, beside the pass's main and
+    // deep launches (it fills their drain); ev_sky after it
+    hipStream_t xs_sky = nullptr;
+    hipEvent_t ev_sky = nullptr;
     bool free_valid[kMaxWs] = {};
     // queue/segment counters of workspace b not known to be zero (set while a render using
     // them is enqueued, cleared once the accumulation that resets them is enqueued after it)
@@ -402,6 +406,11 @@ int rt_scene_destroy(rt_scene *sc)
         if (sc->ev_main[b]) (void)hipEventDestroy(sc->ev_main[b]);
     }
     if (sc->ev_tail) (void)hipEventDestroy(sc->ev_tail);
+    if (sc->xs_sky) {
+        (void)hipStreamSynchronize(sc->xs_sky);
+        (void)hipStreamDestroy(sc->xs_sky);
+    }
+    if (sc->ev_sky) (void)hipEventDestroy(sc->ev_sky);
     for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr, sc->wq})
         if (p) (void)hipFree(p);
     for (float *p : sc->slots)
@@ -537,7 +546,9 @@ int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_ma
                 hipEventCreateWithFlags(&sc->ev_free[b], hipEventDisableTiming) != hipSuccess)
                 rc = fail(RT_ERR_DEVICE, "rt_scene_create: stream/event creation failed");
         }
-        if (rc == RT_OK && hipEventCreateWithFlags(&sc->ev_tail, hipEventDisableTiming) != hipSuccess)
+        if (rc == RT_OK && (hipEventCreateWithFlags(&sc->ev_tail, hipEventDisableTiming) != hipSuccess ||
+                            hipEventCreateWithFlags(&sc->ev_sky, hipEventDisableTiming) != hipSuccess ||
+                            hipStreamCreateWithFlags(&sc->xs_sky, hipStreamNonBlocking) != hipSuccess))
             rc = fail(RT_ERR_DEVICE, "rt_scene_create: event creation failed");
     }
     if (rc == RT_OK) {
@@ -1037,6 +1048,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         // kernel, the positions before the sky tiles'
         const uint64_t n_samples = n_pixels * (s1 - s0);
         k.n_items = static_cast<uint32_t>((ordered && sky_kernel ? sky_pos0 : n_pixels) * slot_rows(s0, s1, pass_pairs));
+        k.n_slots = static_cast<uint32_t>(n_pixels * slot_rows(s0, s1, pass_pairs));
         const uint32_t grid = static_cast<uint32_t>(
             std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(pass_pairs ? occ_pr : occ, in_flight, bufs, n_samples)) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
@@ -1210,9 +1222,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) stats_waves = dgrid * static_cast<uint32_t>(wpb);
             }
         }
+        bool sky_aside = false;  // the sky kernel on its own stream (then the accumulation waits for ev_sky)
         if (sky_kernel && s1 == P.spp) {
             // the sky tiles' pixels, every sample of the frame; position i's sum to its sample-0
-            // slot (which no pass of these groups uses), read by this pass's accumulation
+            // slot (which no pass of these groups uses), read by this pass's accumulation. A pass
+            // issued alone runs it on a stream of its own, after the workspace is free: it starts
+            // as the main launch's workgroups retire and fills the GPU beside the main launch's
+            // drain and the deep launch; beside other renders it follows the pass on its stream
             rt::KSky ks{};
             ks.fc = k.fc;
             ks.block_perm = k.block_perm;
@@ -1220,7 +1236,20 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             ks.n_pix = k.n_pixels - sky_pos0;
             ks.sums = k.slots + 3u * static_cast<size_t>(sky_pos0);
             ks.segments = k.segments;
-            RT_HIP(rt::launch_sky(ks, xst));
+            sky_aside = pipe && !in_flight && !(O.diag & RT_DIAG_SKY_SERIAL);
+            if (sky_aside) {
+                if (sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(sc->xs_sky, sc->ev_free[wb], 0));
+                // (the counters it adds to are this pass's: zeroed on xst before the main launch)
+                if (ks.segments) {
+                    if (!sc->ev_main[wb]) RT_HIP(hipEventCreateWithFlags(&sc->ev_main[wb], hipEventDisableTiming));
+                    if (!two_part) RT_HIP(hipEventRecord(sc->ev_main[wb], xst));
+                    RT_HIP(hipStreamWaitEvent(sc->xs_sky, sc->ev_main[wb], 0));
+                }
+                RT_HIP(rt::launch_sky(ks, sc->xs_sky));
+                RT_HIP(hipEventRecord(sc->ev_sky, sc->xs_sky));
+            } else {
+                RT_HIP(rt::launch_sky(ks, xst));
+            }
         }
         if (variant == rt::V_STATS_LDS) sc->dbg_waves = stats_waves;
         if (s1 == P.spp) RT_HIP(hipEventRecord(sc->ev_end[ring], xst));
@@ -1277,6 +1306,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             a.part = 3;
         }
         if (pipe) RT_HIP(hipStreamWaitEvent(st, sc->ev_done[wb], 0));
+        if (sky_aside) RT_HIP(hipStreamWaitEvent(st, sc->ev_sky, 0));
         RT_HIP(rt::launch_accumulate(a, st));
         sc->ctr_dirty[wb] = false;
         if (pipe) {

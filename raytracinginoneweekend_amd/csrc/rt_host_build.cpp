@@ -89,7 +89,7 @@ int check_options(const rt_options &o)
     if (o.cluster_size < 4 || o.cluster_size > 64 || o.cluster_size % 4) return bad("cluster_size (4..64, multiple of 4)");
     if (o.transpose_max > 16) return bad("transpose_max (0..16)");
     if (o.wave_queue_rays < 64) return bad("wave_queue_rays (>= 64)");
-    if (o.diag & ~((RT_DIAG_SKY_IN_MAIN << 1) - 1u)) return bad("diag (unknown bit)");
+    if (o.diag & ~((RT_DIAG_SKY_SERIAL << 1) - 1u)) return bad("diag (unknown bit)");
     if ((o.diag & RT_DIAG_SHADE_LDS) && (o.diag & RT_DIAG_SHADE_GLOBAL)) return bad("diag (shade_lds with shade_global)");
     return RT_OK;
 }
@@ -104,7 +104,7 @@ int parse_options(const char *text, rt_options &o)
         {"standin_transport", RT_DIAG_STANDIN_TRANSPORT}, {"unbounded_nb", RT_DIAG_UNBOUNDED_NB},
         {"no_pairs", RT_DIAG_NO_PAIRS}, {"pairs", RT_DIAG_PAIRS}, {"in_flight", RT_DIAG_IN_FLIGHT},
         {"natural_order", RT_DIAG_NATURAL_ORDER}, {"no_sky", RT_DIAG_NO_SKY}, {"lone_split", RT_DIAG_LONE_SPLIT},
-        {"sky_in_main", RT_DIAG_SKY_IN_MAIN}};
+        {"sky_in_main", RT_DIAG_SKY_IN_MAIN}, {"sky_serial", RT_DIAG_SKY_SERIAL}};
     rt_options n = o;
     std::string all(text ? text : "");
     for (char &c : all)

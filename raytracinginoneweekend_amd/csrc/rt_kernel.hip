@@ -1236,7 +1236,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
             float *dst;
             if constexpr (DEEP) {
                 const uint32_t role = ls >> 30;
-                dst = P.slots + (size_t)checked<STATS>(pix, P.n_items, BC_SLOT, p.dbg) * 3u;
+                dst = P.slots + (size_t)checked<STATS>(pix, P.n_slots, BC_SLOT, p.dbg) * 3u;
                 if (role == kRolePartnerDone) {
                     // the partner ended in the main launch and left its colour in the slot
                     // (IEEE addition is commutative: the order of the pair's two terms is moot)
@@ -1282,7 +1282,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                         if (STATS) ++dbg.ev[EV_PAIR_SUM];
                     }
                 }
-                dst = P.slots + (size_t)checked<STATS>(slot, P.n_items, BC_SLOT, p.dbg) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
+                dst = P.slots + (size_t)checked<STATS>(slot, P.n_slots, BC_SLOT, p.dbg) * 3u;  // < 2^29: one pass holds <= 2 GiB of slots
             }
             dst[0] = col.x;
             dst[1] = col.y;
@@ -1447,7 +1447,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                                 link = (kRoleBothSecond << 30) | j1;
                                 P.deep.link[j1] = (kRoleBothFirst << 30) | j;
                             } else {  // the first's colour, parked in the lane's LDS words, to the slot
-                                float *dst = P.slots + (size_t)checked<STATS>(slot, P.n_items, BC_SLOT, p.dbg) * 3u;
+                                float *dst = P.slots + (size_t)checked<STATS>(slot, P.n_slots, BC_SLOT, p.dbg) * 3u;
                                 dst[0] = park(0, sl);
                                 dst[1] = park(1, sl);
                                 dst[2] = park(2, sl);

@@ -191,12 +191,12 @@ enum rt_diag {
                                           that plan that must not depend on timing             */
     RT_DIAG_NATURAL_ORDER = 1u << 14,   /* items dealt in the pixels' natural tile order (no
                                           tile classes, no sky path)           */
-    RT_DIAG_NO_SKY = 1u << 15,          /* tile classes order the dealing, but samples of tiles
-                                          proven to reach the sky trace their segment          */
-    RT_DIAG_LONE_SPLIT = 1u << 16,      /* split a lone pass dealt by tile classes as well      */
-    RT_DIAG_SKY_IN_MAIN = 1u << 17,     /* the proven sky tiles dealt last by the main launch
-                                          (no closest hit) instead of the sky kernel            */
-    RT_DIAG_SKY_SERIAL = 1u << 18       /* a lone pass's sky kernel after its main and deep
+    RT_DIAG_NO_SKY = 1u << 15,          /* tile classes order the dealing, but the tiles proven
+                                          to send every primary ray to the sky are dealt last by
+                                          the main launch (traced) instead of the sky kernel   */
+    RT_DIAG_LONE_UNSPLIT = 1u << 16,    /* a lone pass dealt by tile classes is not split (its
+                                          trapped paths start in its first items)              */
+    RT_DIAG_SKY_SERIAL = 1u << 17       /* a lone pass's sky kernel after its main and deep
                                           launches on their stream (not beside them)           */
 };
 int rt_options_default(rt_options *out);

@@ -80,8 +80,8 @@ RT_DIAG = {
     "ieee_roots": 1 << 0, "no_shortcut": 1 << 1, "no_neighbours": 1 << 2, "no_root_box": 1 << 3,
     "shade_lds": 1 << 4, "shade_global": 1 << 5, "stats": 1 << 6, "stats_deep_only": 1 << 7, "verbose": 1 << 8,
     "standin_transport": 1 << 9, "unbounded_nb": 1 << 10, "no_pairs": 1 << 11, "pairs": 1 << 12,
-    "in_flight": 1 << 13, "natural_order": 1 << 14, "no_sky": 1 << 15, "lone_split": 1 << 16,
-    "sky_in_main": 1 << 17, "sky_serial": 1 << 18,
+    "in_flight": 1 << 13, "natural_order": 1 << 14, "no_sky": 1 << 15, "lone_unsplit": 1 << 16,
+    "sky_serial": 1 << 17,
 }
 
 

@@ -144,17 +144,11 @@ struct KParams {
     // takes group g + 1. One group (natural order): item J = slot J.
     const uint32_t *block_perm;
     uint32_t n_groups;          // 1: natural order, 3: tile classes
-    uint32_t sky_grp;           // the group of the proven sky tiles (kItSky), 3 = none
     uint32_t grp_pix[4];
     uint32_t grp_items[3];
     uint32_t grp_blocks[3];     // (natural order: n_blocks, the last one possibly partial)
     UDiv div_grp[3];            // division by group g's position count
 };
-
-// the main launch's item word (below kItSlot: the slot) of a pass dealt by tile classes: the
-// sample's tile is proven to send every primary ray to the sky (single samples only: the pair
-// instantiation uses this bit as kItFirstDeep)
-constexpr uint32_t kItSky = 1u << 30;
 
 // V_STATS_LDS: every lane-computed index into the scene blob, the slots and the deep queue is
 // checked against its bound before use; the first violation is recorded in dbg[kDbgError] as

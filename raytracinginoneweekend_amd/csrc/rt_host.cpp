@@ -1000,7 +1000,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
     const rt_scene::Order *ord = nullptr;
     if (order_ok && !pairs)
         if (int rc = pass_order(sc, *camera, k, &ord); rc) return rc;
-    const bool sky_kernel = ord && ord->d_perm && ord->t.n_sky && !(O.diag & (RT_DIAG_NO_SKY | RT_DIAG_SKY_IN_MAIN));
+    // (max_depth 0: every sample's colour is 0, main.cxx:74, not the sky's)
+    const bool sky_kernel = ord && ord->d_perm && ord->t.n_sky && P.max_depth > 0 && !(O.diag & RT_DIAG_NO_SKY);
     const uint32_t sky_pos0 = sky_kernel ? static_cast<uint32_t>(64u * (ord->t.perm.size() - ord->t.n_sky)) : k.n_pixels;
     const uint32_t ring = static_cast<uint32_t>(sc->calls % rt_scene::kRing);
     ++sc->calls;
@@ -1055,7 +1056,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.guided_l2b = guided_l2b(grid * 4u, in_flight);
         k.block_perm = nullptr;
         k.n_groups = 1;
-        k.sky_grp = 3;
         k.grp_blocks[0] = k.n_blocks;
         k.grp_items[0] = k.n_items;
         k.grp_pix[0] = 0;
@@ -1076,9 +1076,8 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 k.grp_blocks[g] = static_cast<uint32_t>(nbl[g] * S);  // nbl[g] blocks per sample
                 k.div_grp[g] = make_udiv(static_cast<uint32_t>(std::max<uint64_t>(64u * nbl[g], 1u)));
             }
-            if (!(O.diag & RT_DIAG_NO_SKY) && nbl[2]) k.sky_grp = 2;
             sc->used_lead = t.n_lead;
-            sc->used_sky = k.sky_grp == 2 || sky_kernel ? t.n_sky : 0u;
+            sc->used_sky = sky_kernel ? t.n_sky : 0u;
         } else {
             sc->used_lead = sc->used_sky = 0;
         }
@@ -1087,10 +1086,10 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         k.deep_mode = 0;
         bool two_part = false;
         uint32_t stats_waves = 0;  // the instrumented build: waves of the launch the counters cover
-        // a lone pass dealt by tile classes is not split: its trapped paths start in its first
-        // items and end inside the bulk of the launch
+        // (diag lone_unsplit: a lone pass dealt by tile classes is not split, its trapped paths
+        // starting in its first items; slower, the accumulation then waits for the whole launch)
         if (may_split && (n_samples >= O.deep_min_items || in_flight) &&
-            (in_flight || !ordered || (O.diag & RT_DIAG_LONE_SPLIT))) {
+            (in_flight || !ordered || !(O.diag & RT_DIAG_LONE_UNSPLIT))) {
             const uint32_t rcap = deep_region_cap(n_samples), cap = 8u * rcap;
             const size_t px_bytes = deep_px_bytes(n_pixels);
             bool fresh = false;

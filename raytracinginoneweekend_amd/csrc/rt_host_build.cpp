@@ -103,8 +103,8 @@ int parse_options(const char *text, rt_options &o)
         {"stats_deep_only", RT_DIAG_STATS_DEEP_ONLY}, {"verbose", RT_DIAG_VERBOSE},
         {"standin_transport", RT_DIAG_STANDIN_TRANSPORT}, {"unbounded_nb", RT_DIAG_UNBOUNDED_NB},
         {"no_pairs", RT_DIAG_NO_PAIRS}, {"pairs", RT_DIAG_PAIRS}, {"in_flight", RT_DIAG_IN_FLIGHT},
-        {"natural_order", RT_DIAG_NATURAL_ORDER}, {"no_sky", RT_DIAG_NO_SKY}, {"lone_split", RT_DIAG_LONE_SPLIT},
-        {"sky_in_main", RT_DIAG_SKY_IN_MAIN}, {"sky_serial", RT_DIAG_SKY_SERIAL}};
+        {"natural_order", RT_DIAG_NATURAL_ORDER}, {"no_sky", RT_DIAG_NO_SKY}, {"lone_unsplit", RT_DIAG_LONE_UNSPLIT},
+        {"sky_serial", RT_DIAG_SKY_SERIAL}};
     rt_options n = o;
     std::string all(text ? text : "");
     for (char &c : all)

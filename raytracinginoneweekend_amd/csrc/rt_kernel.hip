@@ -971,7 +971,6 @@ __device__ __forceinline__ void render_body(const KParams &p)
     uint32_t cnext = 0, cend = 0;
     // the main launch: the chunk's items [cnext, run_end) lie in one sample, at slots run_base + ...
     uint32_t run_end = 0, run_base = 0;
-    bool run_sky = false;  // ... of the proven sky tiles (kItSky)
     bool exhausted = false;
 
     // lane state: the lane's item is one sample (pixel enumeration index, sample of the pass)
@@ -1054,7 +1053,8 @@ __device__ __forceinline__ void render_body(const KParams &p)
         if (STATS && need && !exhausted && lane == 0) ++dbg_refills;
         while (need && !exhausted) {
             RT_EV(EV_REFILL_TRIP);
-            if (!DEEP && cnext < cend && cnext >= run_end) goto run;  // the chunk's next sample
+            // (the main launch: run_end <= cend, so a finished chunk is a finished run)
+            if (DEEP ? cnext >= cend : cnext >= run_end) {
             if (cnext >= cend) {
                 uint32_t c = 0;
                 if constexpr (DEEP) {
@@ -1137,7 +1137,6 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 cend = __builtin_amdgcn_readfirstlane(min(64u * (qb0 + S(c + 1u)), GI));
                 }
             }
-        run:
             if constexpr (!DEEP) {
                 // the chunk's run within one sample: group grp's item J is sample J / ng at
                 // position p0 + J % ng, slot [sample][position] (sample-major over the pass's
@@ -1152,7 +1151,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 const uint32_t sj = __builtin_amdgcn_readfirstlane(udiv(cnext, dv));
                 run_end = __builtin_amdgcn_readfirstlane(min(cend, (sj + 1u) * ng));
                 run_base = __builtin_amdgcn_readfirstlane(sj * P.n_pixels + p0 + (cnext - sj * ng));
-                run_sky = grp == P.sky_grp;
+            }
             }
         deal:
             const uint32_t avail = (DEEP ? cend : run_end) - cnext;
@@ -1198,7 +1197,6 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     HID(sl) = hid;
                 } else {
                     it = I;  // a pair item (the pass's full blocks) or a single tail sample; its slot
-                    if (!PAIRS && run_sky) it |= kItSky;
                     alive = fresh = true;
                 }
             }
@@ -1481,12 +1479,6 @@ __device__ __forceinline__ void render_body(const KParams &p)
 
         // ---- closest hit of one segment for every live lane -----------------------------
         const bool seg = alive && !defer && depth < P.max_depth;  // depth check: main.cxx:74
-        // the segments that test spheres: all but the primary rays of the tiles proven to send
-        // every primary ray to the sky (kItSky), whose segment meets no sphere:
-        // they skip the closest-hit test and take the sky colour directly (a wave of them alone
-        // runs no test at all; beside other lanes, they neither walk nor find a candidate in the
-        // always-tested spheres, by the same proof)
-        auto sky_ray = [&]() { return !DEEP && !PAIRS && depth == 0u && (it & kItSky) != 0u; };
         // |d|^2 (raytracer.hxx:56) and its refined reciprocal for this segment's roots; the sky
         // below reuses both (unit_direction's length is sqrt of the same sum)
         const float a = d.x * d.x + d.y * d.y + d.z * d.z;
@@ -1501,7 +1493,7 @@ __device__ __forceinline__ void render_body(const KParams &p)
             if (ballot(seg && hid != ~0u))
                 key0 = hint_candidate<FAST, STATS>(seg && hid != ~0u, PN(sl), hid, NB(sl), geo, sidx, o, d, rd, P.iso,
                                                    skip, P.n_geo, P.diag_unbounded_nb, p.dbg);
-            const bool walk = seg && !skip && !sky_ray();
+            const bool walk = seg && !skip;
             const uint64_t wm = ballot(walk);
             if (STATS && first_active_lane()) {
                 dbg.ev[EV_ISO_LANES] += (uint32_t)__popcll(segm & ~wm);
@@ -1517,16 +1509,16 @@ __device__ __forceinline__ void render_body(const KParams &p)
                 if (lane == 0 && wm) ++dbg_walks;  // iterations in which the wave walked
                 if (lane == 0 && nh) ++dbg_walks_nohint;
             }
-            // (the lanes that skip the walk through the shortcut still test the always-tested spheres)
-            if (DEEP || (wm | ballot(skip))) h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);
+            h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, walk, wm, tw, key0);
             if (!seg) h = Hit{kNoHit};
         } else if (seg) {
             h = closest_hit<FAST, CULL, STATS, COUNT>(P, geo, sidx, clus, o, d, rd, dbg, wt, true, segm, nullptr, no_hit());
         }
         stamp(2);
-        if (COUNT) {
-            wt.add_seg(lanes(seg));  // segments of this iteration (main.cxx:74 passed)
-            wt.add_sph((uint64_t)lanes(seg && !sky_ray()) * P.n_always);  // the always-tested spheres, executed
+        {
+            const uint32_t ns = lanes(seg);  // segments of this iteration (main.cxx:74 passed)
+            wt.add_seg(ns);
+            wt.add_sph((uint64_t)ns * P.n_always);
         }
 
         // ---- shading: the hit of every live lane -----------------------------------------

@@ -209,7 +209,7 @@ def test_options_defaults_and_parse():
     ("max_pass_bytes=0", "max_pass_bytes"), ("max_pass_bytes=4294967296", "max_pass_bytes"),
     ("ring_pass_bytes=11", "ring_pass_bytes"), ("ring_pass_bytes=4294967296", "ring_pass_bytes"),
     ("cluster_size=6", "cluster_size"), ("cluster_size=68", "cluster_size"), ("transpose_max=17", "transpose_max"),
-    ("wave_queue_rays=10", "wave_queue_rays"), ("diag=524288", "diag"), ("shade_lds=1,shade_global=1", "diag"),
+    ("wave_queue_rays=10", "wave_queue_rays"), ("diag=262144", "diag"), ("shade_lds=1,shade_global=1", "diag"),
     ("bogus=1", "bogus"), ("render_streams", "key=value"), ("render_streams=-1", "render_streams"),
     ("render_streams=x", "render_streams"), ("stats=2", "stats"), ("deep_split=4294967296", "deep_split")])
 def test_options_rejected_with_the_field_named(text, field):

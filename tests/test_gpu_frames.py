@@ -457,8 +457,7 @@ def test_lone_deep_launch_static_dealing_runs(opts):
     (8 | 16); frames in flight take the 4-wave launch (4). Both equal the unsplit render bit for
     bit, with the same segment counts (no test checked that the static path ran)."""
     torch = pytest.importorskip("torch")
-    # (lone_split: a lone pass dealt by tile classes is not split otherwise, DESIGN.md §4.7)
-    opts.set(deep_min_items=0, shade_global=True, lone_split=True)
+    opts.set(deep_min_items=0, shade_global=True)
     s, m = G.scene("huge")
     W, H, spp = 640, 360, 64
     cam = rt.Camera.default(W, H)
@@ -695,15 +694,15 @@ def test_scene_at_the_lds_limit_renders_or_is_refused():
         _bits_equal(got, want, "culled at the LDS limit")
 
 
-@pytest.mark.parametrize("order", ["classes", "sky_in_main", "no_sky", "natural_order"])
+@pytest.mark.parametrize("order", ["classes", "sky_serial", "no_sky", "natural_order"])
 def test_dealing_orders_keep_the_bits(order, opts):
     """Passes dealt by tile classes (lead tiles first; the proven sky tiles by the
-    sky kernel, or dealt last by the main launch without a closest-hit test, or traced), and in
-    the natural order render the same bits as the oracle: a lone frame (not split), frames in
+    sky kernel, beside the main launch or after it, or traced by the main launch), and in
+    the natural order render the same bits as the oracle: a lone frame (split), frames in
     flight (split, ring passes), an interleaved row share, fast-math against its own natural
     order, and the corrected camera. rt_scene_usage reports the classes that were used."""
     torch = pytest.importorskip("torch")
-    diag = {"classes": {}, "sky_in_main": dict(sky_in_main=True), "no_sky": dict(no_sky=True),
+    diag = {"classes": {}, "sky_serial": dict(sky_serial=True), "no_sky": dict(no_sky=True),
             "natural_order": dict(natural_order=True)}[order]
     opts.set(deep_min_items=0, **diag)
     s, m = G.scene("huge")
@@ -728,9 +727,9 @@ def test_dealing_orders_keep_the_bits(order, opts):
             assert u["lead_tiles"] == 0 and u["sky_tiles"] == 0, u
         elif mode == 0:
             assert u["lead_tiles"] > 0, u
-            assert (u["sky_tiles"] > 0) == (order in ("classes", "sky_in_main")), u
-    # the lone 320x176 frame is not split when dealt by classes
-    assert (used[0]["split_passes"] == 0) == (order != "natural_order"), used[0]
+            assert (u["sky_tiles"] > 0) == (order in ("classes", "sky_serial")), u
+    # the lone 320x176 frame is split (deep_min_items 0), in every order
+    assert used[0]["split_passes"] == 1, used[0]
     # fast-math: the classes and the sky path change no bit of its own result either
     W, H, spp = 320, 176, 8
     p = rt.make_params(W, H, spp, 64, 5, fast_math=True)

@@ -1564,9 +1564,11 @@ int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material 
     uint64_t *d_seg = cx.d_seg;
     hipEvent_t e0 = cx.e0, e1 = cx.e1;
     if (rc == RT_OK && (P.flags & RT_FLAG_FULL_FRAME)) chk(hipMemsetAsync(d_rgb, 0, n_values * 4, nullptr), "hipMemset");
-    if (rc == RT_OK) chk(hipMemsetAsync(d_seg, 0, 24, nullptr), "hipMemset");
+    // the work counters (rt_stats) come from the counting instantiation of the kernels, slower than
+    // the product's: only when the caller asks for them (rt::render_impl does not, as cuda_impl)
+    if (rc == RT_OK && stats) chk(hipMemsetAsync(d_seg, 0, 24, nullptr), "hipMemset");
     if (rc == RT_OK) chk(hipEventRecord(e0, nullptr), "hipEventRecord");
-    if (rc == RT_OK) rc = rt_render_device(sc, camera, params, d_rgb, nullptr, d_seg);
+    if (rc == RT_OK) rc = rt_render_device(sc, camera, params, d_rgb, nullptr, stats ? d_seg : nullptr);
     if (rc == RT_OK) chk(hipEventRecord(e1, nullptr), "hipEventRecord");
     if (rc == RT_OK && u8_out) rc = rt_epilogue_rgb8_device(d_rgb, d_u8, n_values / 3, nullptr);
     uint64_t segs[3] = {0, 0, 0};
@@ -1574,7 +1576,7 @@ int render_host(const rt_sphere *spheres, uint32_t n_spheres, const rt_material 
     // the copies on the null stream follow the render; the last one returns when all is done
     if (rc == RT_OK && rgb_out) chk(hipMemcpy(rgb_out, d_rgb, n_values * 4, hipMemcpyDeviceToHost), "hipMemcpy");
     if (rc == RT_OK && u8_out) chk(hipMemcpy(u8_out, d_u8, n_values, hipMemcpyDeviceToHost), "hipMemcpy");
-    if (rc == RT_OK) chk(hipMemcpy(segs, d_seg, 24, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (rc == RT_OK && stats) chk(hipMemcpy(segs, d_seg, 24, hipMemcpyDeviceToHost), "hipMemcpy");
     if (rc == RT_OK) chk(hipDeviceSynchronize(), "render");
     if (rc == RT_OK) chk(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
     if (rc != RT_OK) {

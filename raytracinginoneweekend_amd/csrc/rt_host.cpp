@@ -97,6 +97,12 @@ float guided_l2b(uint32_t total_waves, bool in_flight)
 constexpr uint64_t kShortPassItems = 32ull << 20;
 // the deep launch of a lone pass stages the shading records in LDS (A/B build switch)
 // lone split passes accumulate in two parts, the first beside the deep launch (A/B build switch)
+#ifndef RT_LONE_SKY_ROOM
+#define RT_LONE_SKY_ROOM -1  // -1: by the sky's share of the pass (see the main launch's grid)
+#endif
+#ifndef RT_PRIO_LONG  // A/B build switch: KParams::prio_depth for lone unsplit passes
+#define RT_PRIO_LONG 1
+#endif
 #ifndef RT_TWO_PART
 #define RT_TWO_PART 1
 #endif
@@ -1050,8 +1056,20 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         const uint64_t n_samples = n_pixels * (s1 - s0);
         k.n_items = static_cast<uint32_t>((ordered && sky_kernel ? sky_pos0 : n_pixels) * slot_rows(s0, s1, pass_pairs));
         k.n_slots = static_cast<uint32_t>(n_pixels * slot_rows(s0, s1, pass_pairs));
+        int wg_cu = grid_wg_per_cu(pass_pairs ? occ_pr : occ, in_flight, bufs, n_samples);
+        // A lone pass whose sky kernel runs beside it: the main launch's workgroups fill every
+        // CU's registers (72 VGPRs x 7 waves per SIMD), so the sky kernel would start only as they
+        // retire and end the frame after them. The main launch leaves room in proportion to the
+        // sky's share of the pixels (config 3, 73% sky: 2 of 7 workgroups per CU; lone frame
+        // 2.466-2.474 ms vs 2.528-2.547 with none, 2.474-2.495 with 1; period unchanged;
+        // profiles/r06/ab/sky_room.txt). RT_LONE_SKY_ROOM >= 0 (A/B build switch) fixes it.
+        if (!in_flight && sky_kernel && ordered && s1 == P.spp && pipe && !(O.diag & RT_DIAG_SKY_SERIAL)) {
+            const double sky_frac = 1.0 - static_cast<double>(sky_pos0) / static_cast<double>(n_pixels);
+            const int room = RT_LONE_SKY_ROOM >= 0 ? RT_LONE_SKY_ROOM : static_cast<int>(wg_cu * sky_frac * 0.4 + 0.5);
+            wg_cu = std::max(1, wg_cu - room);
+        }
         const uint32_t grid = static_cast<uint32_t>(
-            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(grid_wg_per_cu(pass_pairs ? occ_pr : occ, in_flight, bufs, n_samples)) * sc->cu_count, (k.n_items + 255u) / 256u)));
+            std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(wg_cu) * sc->cu_count, (k.n_items + 255u) / 256u)));
         k.n_blocks = (k.n_items + 63u) / 64u;
         k.guided_l2b = guided_l2b(grid * 4u, in_flight);
         k.block_perm = nullptr;
@@ -1084,6 +1102,7 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
         k.deep_depth = 0;
         k.deep_mode = 0;
+        k.prio_depth = 0;
         bool two_part = false;
         uint32_t stats_waves = 0;  // the instrumented build: waves of the launch the counters cover
         // (diag lone_unsplit: a lone pass dealt by tile classes is not split, its trapped paths
@@ -1123,6 +1142,10 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             k.deep.rcap = rcap;
             k.deep_depth = deep_split;
             two_part = RT_TWO_PART && pipe && !in_flight;
+        } else if (RT_PRIO_LONG && may_split && !in_flight) {
+            // a lone pass left unsplit (a row share): the waves holding its trapped paths issue
+            // first once a path passes the split depth (rt_kernel.hip render_body)
+            k.prio_depth = deep_split;
         }
         if (O.diag & RT_DIAG_VERBOSE)
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u "

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-frame kernel timeline of lone frames from a rocprofv3 --kernel-trace CSV: for each frame
 (a main render_kernel launch and what follows it) the main, deep and accumulation launches'
-start offsets and durations in microseconds.
+start offsets and durations in microseconds (main, deep, sky, acc).
     python scripts/lone_timeline.py <run_kernel_trace.csv> [...]
 """
 import csv
@@ -15,7 +15,7 @@ for path in sys.argv[1:]:
         name = r["Kernel_Name"]
         t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         short = ("deep" if "render_deep_kernel" in name else "main" if "render_kernel" in name
-                 else "acc" if "accumulate_kernel" in name else None)
+                 else "acc" if "accumulate_kernel" in name else "sky" if "sky_kernel" in name else None)
         if short is None:
             continue
         if short == "main":

@@ -284,19 +284,23 @@ def pmc_fields(path, kernel, config):
 
 
 
-# Issue cost of one wave64 VALU instruction per SIMD, cycles, by PMC class, as measured on gfx950
-# with 8 waves per SIMD (scripts/ubench_int.hip, profiles/r02/ubench_int.txt): plain f32 add/mul/fma
-# and 32-bit integer ops ~2.4 (an SGPR operand, integer multiplies, bfe/add3/lshl_add take ~4.2:
-# the INT32 and F32 classes mix both, so 2.4 is their floor); 64-bit integer ~4.2; transcendental
-# (rcp, sqrt) ~8.2. The VALU count the typed counters leave over is compares, v_cndmask,
-# conversions, min/max/med3, DPP, moves and f64: counted at ~4.2 (moves issue at ~2.3: an
-# estimate, not a measurement of the mix).
-ISSUE_CYCLES = {"plain": 2.4, "int64": 4.2, "trans": 8.2, "other": 4.2}
+# Issue cost of one wave64 VALU instruction per SIMD, cycles, by PMC class. NOMINAL: the ISA's
+# rates on gfx950 (157.3 TF FP32 = 1024 SIMDs x 2.4 GHz x a wave64 FMA every 2 cycles;
+# MI355X_MICROARCH.md): 2 for the f32/int32 classes and for the VALU count the typed counters
+# leave over (compares, v_cndmask, conversions, min/max, DPP, moves), 4 for 64-bit integer, 8 for
+# transcendentals (rcp, sqrt). UBENCH: as measured with 8 waves per SIMD (scripts/ubench_int.hip,
+# profiles/r02/ubench_int.txt): plain ~2.4 (an SGPR operand, integer multiplies, bfe/add3 ~4.2),
+# int64 ~4.2, trans ~8.2, the rest counted at ~4.2. The nominal count is the floor of the frame's
+# VALU issue time; the ubench count overstates it (on config 3 it exceeds the frame period: the
+# isolated rates include dependency stalls that other waves' issue hides in the kernel).
+ISSUE_CYCLES_NOMINAL = {"plain": 2.0, "int64": 4.0, "trans": 8.0, "other": 2.0}
+ISSUE_CYCLES_UBENCH = {"plain": 2.4, "int64": 4.2, "trans": 8.2, "other": 4.2}
 
 
 def issue_roofline(pmc, ms_per_step):
     """The VALU issue roofline: sum over PMC instruction classes of count x
-    measured issue cycles, over 1024 SIMDs x the PMC run's clock x the frame period."""
+    issue cycles, over the issue capacity of one frame period (1024 SIMDs x the PMC run's clock
+    x ms_per_step). issue_frac at the nominal rates, issue_frac_ubench at the measured ones."""
     c = pmc.get("counters", {})
     need = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32",
             "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_TRANS_F32")
@@ -305,21 +309,21 @@ def issue_roofline(pmc, ms_per_step):
     plain = c["SQ_INSTS_VALU_ADD_F32"] + c["SQ_INSTS_VALU_MUL_F32"] + c["SQ_INSTS_VALU_FMA_F32"] + c["SQ_INSTS_VALU_INT32"]
     int64, trans = c["SQ_INSTS_VALU_INT64"], c["SQ_INSTS_VALU_TRANS_F32"]
     other = max(0.0, c["SQ_INSTS_VALU"] - plain - int64 - trans)
-    cyc = (plain * ISSUE_CYCLES["plain"] + int64 * ISSUE_CYCLES["int64"] + trans * ISSUE_CYCLES["trans"]
-           + other * ISSUE_CYCLES["other"])
     cap = 1024 * pmc["clock_ghz"] * 1e9 * ms_per_step * 1e-3
     tot = c["SQ_INSTS_VALU"]
-    # the same at the nominal issue rates (a wave64 VALU instruction over 2 cycles on a SIMD-32,
-    # MI355X_MICROARCH.md; half-rate shapes 4, transcendentals 8)
-    nom = plain * 2.0 + int64 * 4.0 + trans * 8.0 + other * 4.0
-    return {"issue_frac": round(cyc / cap, 4), "issue_frac_nominal": round(nom / cap, 4),
-            "issue_cycles_per_frame": round(cyc),
+
+    def cycles(r):
+        return plain * r["plain"] + int64 * r["int64"] + trans * r["trans"] + other * r["other"]
+
+    nom, ub = cycles(ISSUE_CYCLES_NOMINAL), cycles(ISSUE_CYCLES_UBENCH)
+    return {"issue_frac": round(nom / cap, 4), "issue_frac_ubench": round(ub / cap, 4),
+            "issue_cycles_per_frame": round(nom), "valu_insts_per_frame": round(tot),
             "issue_mix": {"plain_f32_int32": round(plain / tot, 4), "int64": round(int64 / tot, 4),
-                          "trans": round(trans / tot, 4), "other_estimated": round(other / tot, 4)},
-            "issue_model": "cycles/wave-inst: plain 2.4 (floor: SGPR operands and 4.2-cycle integer shapes "
-                           "inside the class are not separable), int64 4.2, trans 8.2, the VALU count the typed "
-                           "counters leave over (compares, selects, conversions, min/max, DPP, moves) 4.2, "
-                           "an estimate; capacity = 1024 SIMDs x the PMC run's clock x ms_per_step"}
+                          "trans": round(trans / tot, 4), "other": round(other / tot, 4)},
+            "issue_model": "wave64 VALU issue cycles per SIMD at the ISA's nominal rates: f32/int32 and the "
+                           "untyped rest 2, int64 4, transcendental 8 (issue_frac, a floor); at the rates "
+                           "measured in isolation 2.4 / 4.2 / 8.2 / 4.2 (issue_frac_ubench, an overstatement); "
+                           "capacity = 1024 SIMDs x the PMC run's clock x ms_per_step"}
 
 
 def dropin_timing(arrays, cam, W, H, spp, depth, seed, repeats=3):

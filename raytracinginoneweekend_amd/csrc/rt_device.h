@@ -130,7 +130,6 @@ struct KParams {
     uint32_t deep_depth;     // 0: no split (and always 0 in the deep launch)
     uint32_t deep_mode;      // the deep launch: the split depth (its paths resume there); 0 otherwise
     uint32_t deep_prio;      // the deep launch's waves at the highest issue priority (s_setprio 3)
-    uint32_t prio_depth;     // unsplit main launch: a wave holding a path this deep issues first (0: off)
     uint32_t deep_static;    // the deep launch deals chunk j to wave j mod (waves of the grid), no atomics
     // instrumented kernel only (V_STATS_LDS): hint_candidate's neighbour slots formed without the
     // lane's own bound (the form before fd383c3), so that the bounds check sees stale words

@@ -100,9 +100,6 @@ constexpr uint64_t kShortPassItems = 32ull << 20;
 #ifndef RT_LONE_SKY_ROOM
 #define RT_LONE_SKY_ROOM -1  // -1: by the sky's share of the pass (see the main launch's grid)
 #endif
-#ifndef RT_PRIO_LONG  // A/B build switch: KParams::prio_depth for lone unsplit passes
-#define RT_PRIO_LONG 1
-#endif
 #ifndef RT_TWO_PART
 #define RT_TWO_PART 1
 #endif
@@ -169,9 +166,8 @@ struct rt_scene {
     hipStream_t xs[kMaxBufs] = {};
     hipEvent_t ev_done[kMaxWs] = {}, ev_free[kMaxWs] = {};
     hipEvent_t ev_main[kMaxWs] = {};  // split passes: after the main launch (created on first use)
-    // the sky kernel of a pass issued alone runs on a stream of its own, beside the pass's main and
-    // deep launches (it fills their drain); ev_sky after it
-    hipStream_t xs_sky = nullptr;
+    // the sky kernel of a pass issued alone runs beside the pass's main and deep launches, on the
+    // next render stream (idle: nothing else runs); ev_sky after it
     hipEvent_t ev_sky = nullptr;
     bool free_valid[kMaxWs] = {};
     // queue/segment counters of workspace b not known to be zero (set while a render using
@@ -412,10 +408,6 @@ int rt_scene_destroy(rt_scene *sc)
         if (sc->ev_main[b]) (void)hipEventDestroy(sc->ev_main[b]);
     }
     if (sc->ev_tail) (void)hipEventDestroy(sc->ev_tail);
-    if (sc->xs_sky) {
-        (void)hipStreamSynchronize(sc->xs_sky);
-        (void)hipStreamDestroy(sc->xs_sky);
-    }
     if (sc->ev_sky) (void)hipEventDestroy(sc->ev_sky);
     for (void *p : {(void *)sc->blob[0], (void *)sc->blob[1], (void *)sc->dbg, (void *)sc->acc, (void *)sc->queue_ctr, sc->wq})
         if (p) (void)hipFree(p);
@@ -553,8 +545,7 @@ int rt_scene_create_ex(const rt_sphere *spheres, uint32_t n_spheres, const rt_ma
                 rc = fail(RT_ERR_DEVICE, "rt_scene_create: stream/event creation failed");
         }
         if (rc == RT_OK && (hipEventCreateWithFlags(&sc->ev_tail, hipEventDisableTiming) != hipSuccess ||
-                            hipEventCreateWithFlags(&sc->ev_sky, hipEventDisableTiming) != hipSuccess ||
-                            hipStreamCreateWithFlags(&sc->xs_sky, hipStreamNonBlocking) != hipSuccess))
+                            hipEventCreateWithFlags(&sc->ev_sky, hipEventDisableTiming) != hipSuccess))
             rc = fail(RT_ERR_DEVICE, "rt_scene_create: event creation failed");
     }
     if (rc == RT_OK) {
@@ -1102,7 +1093,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
         // deep-path split: this workspace's deep queue (its counters in the queue-counter block)
         k.deep_depth = 0;
         k.deep_mode = 0;
-        k.prio_depth = 0;
         bool two_part = false;
         uint32_t stats_waves = 0;  // the instrumented build: waves of the launch the counters cover
         // (diag lone_unsplit: a lone pass dealt by tile classes is not split, its trapped paths
@@ -1142,10 +1132,6 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             k.deep.rcap = rcap;
             k.deep_depth = deep_split;
             two_part = RT_TWO_PART && pipe && !in_flight;
-        } else if (RT_PRIO_LONG && may_split && !in_flight) {
-            // a lone pass left unsplit (a row share): the waves holding its trapped paths issue
-            // first once a path passes the split depth (rt_kernel.hip render_body)
-            k.prio_depth = deep_split;
         }
         if (O.diag & RT_DIAG_VERBOSE)
             std::fprintf(stderr, "[rt] variant=%d cull=%d shade_lds=%u lds=%zu B occ=%d WG/CU cus=%d grid=%u items=%u "
@@ -1244,13 +1230,13 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
                 if (variant == rt::V_STATS_LDS && (O.diag & RT_DIAG_STATS_DEEP_ONLY)) stats_waves = dgrid * static_cast<uint32_t>(wpb);
             }
         }
-        bool sky_aside = false;  // the sky kernel on its own stream (then the accumulation waits for ev_sky)
+        bool sky_aside = false;  // the sky kernel on another stream (then the accumulation waits for ev_sky)
         if (sky_kernel && s1 == P.spp) {
             // the sky tiles' pixels, every sample of the frame; position i's sum to its sample-0
             // slot (which no pass of these groups uses), read by this pass's accumulation. A pass
-            // issued alone runs it on a stream of its own, after the workspace is free: it starts
-            // as the main launch's workgroups retire and fills the GPU beside the main launch's
-            // drain and the deep launch; beside other renders it follows the pass on its stream
+            // issued alone runs it on another stream, after the workspace is free, beside the main
+            // launch (which leaves it room) and the deep launch; beside other renders it follows
+            // the pass on its stream
             rt::KSky ks{};
             ks.fc = k.fc;
             ks.block_perm = k.block_perm;
@@ -1260,15 +1246,21 @@ int render_device_impl(rt_scene *sc, const rt_camera *camera, const rt_params &P
             ks.segments = k.segments;
             sky_aside = pipe && !in_flight && !(O.diag & RT_DIAG_SKY_SERIAL);
             if (sky_aside) {
-                if (sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(sc->xs_sky, sc->ev_free[wb], 0));
+                // the next render stream, not a stream of its own: HIP maps streams to hardware
+                // queues round-robin in creation order, and a ninth stream shared a queue with one
+                // of the render streams, behind whose main launch the sky kernel then waited (one
+                // lone frame in three at 4 queues: 0.83 vs 0.69 ms on the 8-way share). Consecutive
+                // render streams sit on different queues.
+                hipStream_t sky_st = sc->xs[(wb % bufs + 1u) % bufs];
+                if (sc->free_valid[wb]) RT_HIP(hipStreamWaitEvent(sky_st, sc->ev_free[wb], 0));
                 // (the counters it adds to are this pass's: zeroed on xst before the main launch)
                 if (ks.segments) {
                     if (!sc->ev_main[wb]) RT_HIP(hipEventCreateWithFlags(&sc->ev_main[wb], hipEventDisableTiming));
                     if (!two_part) RT_HIP(hipEventRecord(sc->ev_main[wb], xst));
-                    RT_HIP(hipStreamWaitEvent(sc->xs_sky, sc->ev_main[wb], 0));
+                    RT_HIP(hipStreamWaitEvent(sky_st, sc->ev_main[wb], 0));
                 }
-                RT_HIP(rt::launch_sky(ks, sc->xs_sky));
-                RT_HIP(hipEventRecord(sc->ev_sky, sc->xs_sky));
+                RT_HIP(rt::launch_sky(ks, sky_st));
+                RT_HIP(hipEventRecord(sc->ev_sky, sky_st));
             } else {
                 RT_HIP(rt::launch_sky(ks, xst));
             }

@@ -1457,13 +1457,6 @@ __device__ __forceinline__ void render_body(const KParams &p)
                     P.deep.link[j] = link;
                 }
             }
-        } else if (!DEEP && P.prio_depth) {
-            // a pass not split (a lone row share): the paths trapped in glass balls run to
-            // max_depth in this launch, each a chain of ~64 dependent iterations of its wave,
-            // which shares its SIMD with six others; the wave holding such a path issues ahead
-            // of them (the deep launch's waves do the same, KParams::deep_prio)
-            if (ballot(alive && depth >= P.prio_depth)) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(0);
         }
         RT_EV(EV_ITER);
         if (STATS) {

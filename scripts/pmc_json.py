@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ap = argparse.ArgumentParser()
 ap.add_argument("root")
 ap.add_argument("out")
-ap.add_argument("--kernel", default="render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8> + sky_kernel",
+ap.add_argument("--kernel", default="render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8> + sky_kernel<1>",
                 help="kernel names joined by ' + '; the first one's dispatches count the frames")
 ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")

@@ -7,7 +7,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --corrected-steps 0}
+ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --corrected-steps 0 --no-dropin}
+# (--no-dropin: the drop-in timing renders frames through another scene, which the PMC sums would
+# count and frames_issued would not)
 i=0
 while read -r line; do
   [ -z "$line" ] && continue

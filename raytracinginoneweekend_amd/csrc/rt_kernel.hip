@@ -1979,17 +1979,14 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
 // The pixels of the tiles proven to send every primary ray to the sky: each sample is the
 // reference's primary ray (main.cxx:192-200, camera.hxx:46-57) and its colour the sky's
 // (main.cxx:71: background(.5 unit_direction(d).y + 1) times an attenuation of 1, exact), the
-// closest hit being proven empty. A pixel's samples are summed in the blocked order of
-// main.cxx:205's std::reduce: ((c0 + c1) + (c2 + c3)) per block of 4, added to the running sum
-// block after block, then the tail samples one by one; accumulate_kernel divides by spp.
-// PARTS threads share a pixel (lanes 4j .. 4j + PARTS - 1 of the wave): part k traces the k-th
-// run of its blocks (part PARTS - 1 also the tail) — a pixel's 128 samples in one thread would
-// be ~0.3 ms of one wave, and 1.3 rounds of such waves leave the GPU a third busy at the end —
-// part 0 adds its blocks to the running sum as they end, the others park their block sums (and
-// the tail's colours) in LDS, and part 0 then adds those in order: the same additions in the
-// same order as the reference's reduce. A lane makes at most RT_SKY_CAP attempts of its lens
-// draw per iteration and resumes the same sequence in the next, so the wave does not wait for
-// its unluckiest lane's whole rejection run; same draws, same order, same bits.
+// closest hit being proven empty. One thread per pixel, its samples in order, summed in the
+// blocked order of main.cxx:205's std::reduce: ((c0 + c1) + (c2 + c3)) per block of 4, added to
+// the running sum block after block, then the tail samples one by one; accumulate_kernel divides
+// by spp. A lane makes at most RT_SKY_CAP attempts of its lens draw per iteration and resumes
+// the same sequence in the next, so the wave does not wait for its unluckiest lane's whole
+// rejection run; same draws, same order, same bits. (4 threads per pixel with an LDS combine, so
+// that the kernel's last waves end sooner, were not faster: profiles/r06/ab/sky_parts.txt,
+// deep_sky_tail.txt; the kernel is throughput-bound on what the main launch leaves it.)
 // The sky kernel's cap on lens attempts per iteration: an iteration is the sample's start, the
 // attempts and its colour, so a lower cap than the main loop's (whose iterations trace a
 // segment) wastes fewer attempt slots on the lanes that accepted early: per sample, iterations
@@ -1997,13 +1994,10 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const KAccum k)
 #ifndef RT_SKY_CAP
 #define RT_SKY_CAP 2
 #endif
-template <int PARTS>
 __global__ __launch_bounds__(256) void sky_kernel(const KSky p)
 {
-    extern __shared__ float4 sky_lds[];  // [64 pixels][(PARTS - 1) * per_part + 3] block sums / tail colours
     const FrameConsts &fc = p.fc;
-    const uint32_t px_local = threadIdx.x / PARTS, part = threadIdx.x % PARTS;
-    const uint32_t t = blockIdx.x * (256u / PARTS) + px_local;  // the sky pixel
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;  // the sky pixel
     const bool live = t < p.n_pix;
     uint32_t px, rr;
     pixel_of(fc, p.pos0 + (live ? t : 0u), px, rr, p.block_perm);
@@ -2011,18 +2005,14 @@ __global__ __launch_bounds__(256) void sky_kernel(const KSky p)
     const uint64_t inc_data = ((uint64_t)fc.inc_data_hi << 32) | fc.inc_data_lo;
     const uint64_t inc_cam = ((uint64_t)fc.inc_cam_hi << 32) | fc.inc_cam_lo;
     const uint64_t key0 = (uint64_t)(py * fc.W + px) * fc.spp;
-    const uint32_t spp = fc.spp, full_end = spp & ~3u, nb = full_end / 4u;
-    // this part's blocks [b0, b1); the last part also the tail samples [full_end, spp)
-    const uint32_t b0 = nb * part / PARTS, b1 = nb * (part + 1u) / PARTS;
-    const uint32_t per_part = (nb + PARTS - 1u) / PARTS;  // LDS entries per parked part
-    const uint32_t s_end = part == PARTS - 1u ? spp : 4u * b1;
-    float *park = reinterpret_cast<float *>(sky_lds) + 3u * (px_local * ((PARTS - 1u) * per_part + 3u));
+    const uint32_t spp = fc.spp, full_end = spp & ~3u;
     const float fW = fc.fW, fH = fc.fH, rW = fc.rW, rH = fc.rH;
     const bool dw = fc.div_fast & 1u, dh = fc.div_fast & 2u;
     const f3 org = mk(fc.org[0], fc.org[1], fc.org[2]), llc = mk(fc.llc[0], fc.llc[1], fc.llc[2]);
     const f3 hor = mk(fc.hor[0], fc.hor[1], fc.hor[2]), ver = mk(fc.ver[0], fc.ver[1], fc.ver[2]);
-    f3 acc = mk(0.f, 0.f, 0.f), c01 = acc, c2 = acc;
-    uint32_t s = live ? 4u * b0 : s_end;
+    // acc: the running sum; pa: the block's current pair (c0, c0 + c1, c2, c2 + c3); pb: c0 + c1
+    f3 acc = mk(0.f, 0.f, 0.f), pa = acc, pb = acc;
+    uint32_t s = live ? 0u : spp;
     bool started = false;
     uint64_t rc = 0;
     float uu = 0.f, vv = 0.f;
@@ -2033,10 +2023,10 @@ __global__ __launch_bounds__(256) void sky_kernel(const KSky p)
     // so the two products step by M and M^2 (mod 2^64, exact): no multiply per sample
     const uint64_t cd1 = inc_data * (kPcgMul + 1u), cd2 = cd1 * kPcgMul + inc_data, cc = inc_cam * (kPcgMul + 1u);
     const uint64_t mm = kPcgMul * kPcgMul;
-    uint64_t km = (key0 + s) * kPcgMul, kmm = km * kPcgMul;
+    uint64_t km = key0 * kPcgMul, kmm = km * kPcgMul;
     const float ux = div_const((float)px, fW, rW, dw), vy = div_const((float)py, fH, rH, dh);
-    while (ballot(s < s_end)) {
-        if (s < s_end) {
+    while (ballot(s < spp)) {
+        if (s < spp) {
             if (!started) {
                 rc = km + cc;
                 const float xu = fminf((float)pcg_out(km + cd1), 0x1.fffffep31f) * 0x1p-32f;  // canonical()
@@ -2067,55 +2057,32 @@ __global__ __launch_bounds__(256) void sky_kernel(const KSky p)
                 }
                 const float tt = .5f * uy + 1.f;                                    // main.cxx:71
                 const f3 col = mk(1.f, 1.f, 1.f) * (1.f - tt) + mk(.5f, .7f, 1.f) * tt;
-                if (s < full_end) {
-                    const uint32_t j = s & 3u;
-                    if (j == 0u) c01 = col;
-                    else if (j == 1u) c01 = c01 + col;                              // c0 + c1
-                    else if (j == 2u) c2 = col;
-                    else {
-                        const f3 bs = c01 + (c2 + col);                             // (c0+c1)+(c2+c3)
-                        if (part == 0u) {
-                            acc = acc + bs;
-                        } else {
-                            float *e = park + 3u * ((part - 1u) * per_part + (s / 4u - b0));
-                            e[0] = bs.x; e[1] = bs.y; e[2] = bs.z;
-                        }
-                    }
-                } else {  // the tail (the last part)
-                    if (PARTS == 1) {
-                        acc = acc + col;
-                    } else {
-                        float *e = park + 3u * ((PARTS - 1u) * per_part + (s - full_end));
-                        e[0] = col.x; e[1] = col.y; e[2] = col.z;
-                    }
-                }
+                // the blocked sum as selects: pa = c0, c0 + c1, c2, c2 + c3 for s & 3 = 0..3;
+                // pb keeps c0 + c1; the block's (c0 + c1) + (c2 + c3), or a tail colour, folds in
+                const bool tail = s >= full_end;
+                const uint32_t j = s & 3u;
+                const f3 sum = pa + col;
+                const bool odd = !tail && (j & 1u);
+                pa = mk(odd ? sum.x : col.x, odd ? sum.y : col.y, odd ? sum.z : col.z);
+                const bool first_pair = !tail && j == 1u;
+                pb = mk(first_pair ? pa.x : pb.x, first_pair ? pa.y : pb.y, first_pair ? pa.z : pb.z);
+                const bool fold = tail || j == 3u;
+                const f3 add = pb + pa;
+                const f3 fa = acc + mk(tail ? col.x : add.x, tail ? col.y : add.y, tail ? col.z : add.z);
+                acc = mk(fold ? fa.x : acc.x, fold ? fa.y : acc.y, fold ? fa.z : acc.z);
                 ++s;
                 started = false;
             }
         }
     }
-    if (PARTS > 1) {
-        __syncthreads();
-        if (part == 0u && live) {
-            for (uint32_t k = 1; k < (uint32_t)PARTS; ++k)
-                for (uint32_t b = nb * k / PARTS; b < nb * (k + 1u) / PARTS; ++b) {
-                    const float *e = park + 3u * ((k - 1u) * per_part + (b - nb * k / PARTS));
-                    acc = acc + mk(e[0], e[1], e[2]);
-                }
-            for (uint32_t j = full_end; j < spp; ++j) {
-                const float *e = park + 3u * ((PARTS - 1u) * per_part + (j - full_end));
-                acc = acc + mk(e[0], e[1], e[2]);
-            }
-        }
-    }
-    if (part == 0u && live) {
+    if (live) {
         float *o = p.sums + 3u * (size_t)t;
         o[0] = acc.x;
         o[1] = acc.y;
         o[2] = acc.z;
     }
     if (p.segments) {
-        const uint32_t n = lanes(part == 0u && live);
+        const uint32_t n = lanes(live);
         if ((threadIdx.x & 63u) == 0u && n) atomicAdd(p.segments, (unsigned long long)n * spp);
     }
 }
@@ -2472,23 +2439,10 @@ hipError_t launch_accumulate(const KAccum &k, hipStream_t stream)
     return hipGetLastError();
 }
 
-// RT_SKY_PARTS 4 (A/B build switch): 4 parts per pixel when their parked block sums fit 32 KB of
-// LDS per workgroup (64 pixels: spp up to ~336); default one thread per pixel: the kernel runs
-// on what the main launch leaves free and is throughput-bound, and 4 parts were not faster
-// (config 3 lone frame 2.685-2.689 vs 2.619-2.628 ms; profiles/r06/ab/sky_parts.txt)
-#ifndef RT_SKY_PARTS
-#define RT_SKY_PARTS 1
-#endif
 hipError_t launch_sky(const KSky &k, hipStream_t stream)
 {
     if (!k.n_pix) return hipSuccess;
-    const uint32_t nb = (k.fc.spp & ~3u) / 4u, per_part = (nb + 3u) / 4u;
-    const size_t lds4 = 64u * (3u * per_part + 3u) * 12u;
-    if (RT_SKY_PARTS == 4 && lds4 <= 32768u) {
-        hipLaunchKernelGGL(sky_kernel<4>, dim3((k.n_pix + 63u) / 64u), dim3(256), lds4, stream, k);
-    } else {
-        hipLaunchKernelGGL(sky_kernel<1>, dim3((k.n_pix + 255u) / 256u), dim3(256), 0, stream, k);
-    }
+    hipLaunchKernelGGL(sky_kernel, dim3((k.n_pix + 255u) / 256u), dim3(256), 0, stream, k);
     return hipGetLastError();
 }
 

@@ -91,6 +91,39 @@ def test_baseline_frame_stream_matches_reference(cfg):
     assert int(seg[0]) > W * H * spp  # every primary plus its bounces
 
 
+@pytest.mark.parametrize("share", [(2, 1), (4, 2), (8, 0), (8, 7)])
+def test_config3_row_shares_match_reference_rows(share):
+    """Config 3's row shares as bench.py --gpus N renders them (rank r: rows r, r + N, ...): each
+    row of a share must equal the reference's row (its sha256 in tests/golden/fullframe.json):
+    the tile classes and the sky proof over strided rows (row_offset, row_stride), the sky
+    kernel's pixel enumeration through the share's block permutation, a lone frame (its main
+    launch leaving room for the sky kernel on the next render stream), then two back to back."""
+    torch = pytest.importorskip("torch")
+    n, r = share
+    ref = _full_ref("c3")
+    W, H, spp, depth = ref["width"], ref["height"], ref["spp"], ref["depth"]
+    s, m = G.scene(ref["scene"])
+    rows = (H - r + n - 1) // n
+    p = rt.make_params(W, H, spp, depth, ref["seed"], row_offset=r, row_stride=n, num_rows=rows)
+    cam = rt.Camera.default(W, H)
+    ds = rt.DeviceScene((s, m))
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(3)]
+    ds.render(cam, p, outs[0].data_ptr(), stream)
+    torch.cuda.synchronize()
+    sky = ds.usage()["sky_tiles"]
+    for o in outs[1:]:
+        ds.render(cam, p, o.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ds.close()
+    assert sky > 0
+    for k, o in enumerate(outs):
+        img = o.cpu().numpy()
+        bad = [i for i in range(rows)
+               if hashlib.sha256(img[i].tobytes()).hexdigest()[:16] != ref["row_sha256_16"][r + i * n]]
+        assert not bad, f"share {r}/{n} frame {k}: rows differ from the reference: {[r + i * n for i in bad[:8]]}"
+
+
 def test_bounds_checked_frame_stream_c3():
     """Round 4's hipErrorIllegalAddress, pinned. The instrumented kernel
     (options stats=True) checks every lane-computed index into the scene blob, the sample slots

@@ -114,10 +114,14 @@ constexpr uint64_t kShortPassItems = 32ull << 20;
 #ifndef RT_DEEP_STATIC
 #define RT_DEEP_STATIC 1
 #endif
+#ifndef RT_SHORT_OTHERS  // A/B build switch: the divisor for short passes in flight (-1: streams - 1)
+#define RT_SHORT_OTHERS -1
+#endif
 int grid_wg_per_cu(int occ, bool in_flight, uint32_t streams, uint64_t pass_items)
 {
     if (!in_flight) return occ;
-    const int others = pass_items <= kShortPassItems ? std::max(1, static_cast<int>(streams) - 1)
+    const int short_others = RT_SHORT_OTHERS > 0 ? RT_SHORT_OTHERS : std::max(1, static_cast<int>(streams) - 1);
+    const int others = pass_items <= kShortPassItems ? short_others
                                                      : std::min(2, std::max(1, static_cast<int>(streams) - 1));
     return std::max(1, (occ + others - 1) / others);
 }

@@ -727,6 +727,33 @@ def test_scene_at_the_lds_limit_renders_or_is_refused():
         _bits_equal(got, want, "culled at the LDS limit")
 
 
+@pytest.mark.parametrize("spp,depth", [(1, 64), (2, 64), (5, 64), (7, 3), (13, 64), (6, 1)])
+def test_sky_kernel_tail_samples(spp, depth, opts):
+    """The sky kernel's blocked sum with tail samples (spp % 4 != 0: the reduce's tail after the
+    blocks of 4, main.cxx:205) and without full blocks (spp < 4), at small depth limits: frames of
+    the huge scene whose sky tiles it renders, lone (split) and back to back, equal the oracle's."""
+    torch = pytest.importorskip("torch")
+    opts.set(deep_min_items=0)
+    s, m = G.scene("huge")
+    W, H = 192, 96
+    p = rt.make_params(W, H, spp, depth, 31)
+    cam = rt.Camera.default(W, H)
+    want, _ = O.render_f32(s, m, O.camera_default(W, H, 0), p)
+    stream = torch.cuda.current_stream().cuda_stream
+    ds = rt.DeviceScene((s, m))
+    outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda") for _ in range(3)]
+    ds.render(cam, p, outs[0].data_ptr(), stream)
+    torch.cuda.synchronize()
+    sky = ds.usage()["sky_tiles"]
+    for o in outs[1:]:
+        ds.render(cam, p, o.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ds.close()
+    assert sky > 0
+    for k, o in enumerate(outs):
+        _bits_equal(o.cpu().numpy(), want, f"spp {spp} depth {depth} frame {k}")
+
+
 @pytest.mark.parametrize("order", ["classes", "sky_serial", "no_sky", "natural_order"])
 def test_dealing_orders_keep_the_bits(order, opts):
     """Passes dealt by tile classes (lead tiles first; the proven sky tiles by the

@@ -194,14 +194,14 @@ def lib_sha256():
 
 # the timed kernels: rt::render_kernel<0, 7, false, false, false> (main launch, single samples),
 # rt::render_deep_kernel<0, false, false, 4 | 8> (the deep launch of a split pass: 4-wave groups
-# beside other renders, 8-wave groups for a lone pass) and rt::sky_kernel<1> (the tiles proven to send
+# beside other renders, 8-wave groups for a lone pass) and rt::sky_kernel (the tiles proven to send
 # every primary ray to the sky)
 TIMED_KERNEL = ("_ZN2rt13render_kernelILi0ELi7ELb0ELb0ELb0EEEvNS_7KParamsE",
                 "_ZN2rt18render_deep_kernelILi0ELb0ELb0ELi4EEEvNS_7KParamsE",
                 "_ZN2rt18render_deep_kernelILi0ELb0ELb0ELi8EEEvNS_7KParamsE",
-                "_ZN2rt10sky_kernelILi1EEEvNS_4KSkyE")
+                "_ZN2rt10sky_kernelENS_4KSkyE")
 TIMED_KERNEL_NAMES = ("render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8> + "
-                      "sky_kernel<1>")
+                      "sky_kernel")
 
 
 def hashlib_sha256(b):
@@ -277,7 +277,10 @@ def pmc_fields(path, kernel, config):
         return None, "absent"
     if rec.get("kernel") != kernel or rec.get("config") != config:
         return None, "other kernel or workload"
-    if rec.get("kernel_sha256") != kernel_sha256():
+    here = kernel_sha256()
+    if here is None:  # a timed kernel's symbol is missing from the loaded library
+        return None, "timed kernel not found in the library"
+    if rec.get("kernel_sha256") != here:
         return None, "stale: summary of another build of the timed kernel"
     return rec, "current build of the timed kernel"
 

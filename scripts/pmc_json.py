@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ap = argparse.ArgumentParser()
 ap.add_argument("root")
 ap.add_argument("out")
-ap.add_argument("--kernel", default="render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8> + sky_kernel<1>",
+ap.add_argument("--kernel", default="render_kernel<0, 7, false, false, false> + render_deep_kernel<0, false, false, 4|8> + sky_kernel",
                 help="kernel names joined by ' + '; the first one's dispatches count the frames")
 ap.add_argument("--config", default="c3")
 ap.add_argument("--camera", default="reference")
@@ -86,6 +86,8 @@ if missing:
     raise SystemExit(f"missing counters {missing} for kernel {a.kernel!r} under {a.root}")
 from bench import WORKLOAD, kernel_sha256, lib_sha256  # noqa: E402
 
+if kernel_sha256() is None:
+    raise SystemExit("a timed kernel's symbol (bench.TIMED_KERNEL) is missing from the loaded library")
 t = sum(dur) / len(dur)
 cycles = m["GRBM_GUI_ACTIVE"] / 8.0
 rec = {

@@ -14,6 +14,7 @@
 //                                       cache and the options defaults from several threads
 #include <cmath>
 #include <cstdint>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -175,6 +176,31 @@ void check_builders(const std::string &golden)
     }
 }
 
+// tile classes: the frame-sized classification runs on several threads (each
+// writes its own tiles; TSAN checks that), a row share's on one; the frame's is a permutation,
+// the same on every run, with the classes' counts in range
+void check_tiles(const std::string &golden)
+{
+    std::vector<rt_sphere> s;
+    std::vector<rt_material> m;
+    CHECK(load_scene(golden + "/scene_huge_1234.bin", s, m));
+    const rthost::blob_t b = rthost::build_blob(s.data(), static_cast<uint32_t>(s.size()), true, 16);
+    const rthost::scene_geom g = rthost::scene_geometry(s.data(), b);
+    rt_camera cam{};
+    CHECK(rt_camera_default(1280, 720, RT_CAMERA_REFERENCE, &cam) == RT_OK);
+    const rthost::tile_order a = rthost::classify_tiles(cam, 1280, 720, 0, 1, 720, 3u, g);
+    const rthost::tile_order a2 = rthost::classify_tiles(cam, 1280, 720, 0, 1, 720, 3u, g);
+    CHECK(a.perm.size() == 14400u && a.perm == a2.perm && a.n_lead == a2.n_lead && a.n_sky == a2.n_sky);
+    std::vector<uint32_t> sorted = a.perm;
+    std::sort(sorted.begin(), sorted.end());
+    for (uint32_t i = 0; i < sorted.size(); ++i) CHECK(sorted[i] == i);
+    CHECK(a.n_lead >= 161u && a.n_sky >= 10000u && a.n_lead + a.n_sky <= 14400u);
+    // rows 8 j (share 0 of 8; 90 rows): 11 tile rows of 160 tiles (8 x 8 tiles over the packed rows)
+    const rthost::tile_order sh = rthost::classify_tiles(cam, 1280, 720, 0, 8, 90, 3u, g);
+    CHECK(sh.perm.size() == 1800u);  // 1280 x 90 / 64 blocks
+    CHECK(sh.n_sky > 0u && sh.n_sky < 1800u);
+}
+
 void check_divisions()
 {
     std::mt19937 rng(9);
@@ -310,6 +336,7 @@ int main(int argc, char **argv)
         check_scene_generators(golden);
         check_cameras();
         check_builders(golden);
+        check_tiles(golden);
         check_divisions();
         check_options();
         check_ppm(golden);

@@ -118,4 +118,9 @@ void cuda_impl(std::uint32_t width, std::uint32_t height, std::vector<Texel> &im
           "rt_render_cuda_impl");
 }
 
+// The synchronous calls above keep one context per device between calls (the scene's device
+// copy, streams, workspaces), so that a frame per call costs the frame. Frees it
+// (process exit does too).
+inline void release_cached() { check(rt_release_cached(), "rt_release_cached"); }
+
 } // namespace rt
